@@ -1,0 +1,238 @@
+"""CPU parity oracle for the dmmt JPEG encode path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may
+import this package.  The product (``dmmt-jpeg-encoder_amd/``) never imports or
+links it; the product path fails loudly when its HIP library is missing.
+
+Contents
+  * ``cpu_ref`` (C, cpu_ref.c): stage-by-stage restatement of the reference's
+    Rust encoder, built by oracle/Makefile into oracle/build/libcpu_ref.so.
+  * ``np_ref`` (numpy/pure Python, np_ref.py): a second, independent
+    restatement used to cross-check cpu_ref.
+  * ``jpeg_scan``: a baseline-JPEG Huffman *decoder* to coefficients, used to
+    pin the back half against the reference-produced file
+    /root/reference/tests/output_image_2.jpg (committed as a fixture).
+
+Parity is pinned by the reference's own known-answer tests (ported as data in
+tests/test_oracle_kat.py) and by the two reference outputs in the reference's
+tests/ directory; see DESIGN.md "Oracle".
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libcpu_ref.so")
+_lib = None
+
+P444, P422, P420 = 0, 1, 2
+PRESET_NAMES = {"P444": P444, "P422": P422, "P420": P420}
+
+
+class RefOptions(ctypes.Structure):
+    _fields_ = [
+        ("preset", ctypes.c_int),
+        ("bits_per_channel", ctypes.c_int),
+        ("luma_q", ctypes.c_uint8 * 64),
+        ("chroma_q", ctypes.c_uint8 * 64),
+    ]
+
+
+def build() -> str:
+    """Compile cpu_ref.c (gcc, -ffp-contract=off)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        f32, u16, u8, i32 = ctypes.c_float, ctypes.c_uint16, ctypes.c_uint8, ctypes.c_int
+        vp = ctypes.c_void_p
+        L.ref_normalize.restype = f32
+        L.ref_normalize.argtypes = [u16, u16]
+        L.ref_rgb_to_ycbcr.argtypes = [f32, f32, f32, ctypes.POINTER(f32)]
+        L.ref_fast_arai.argtypes = [ctypes.POINTER(f32), i32]
+        L.ref_dct_block.argtypes = [ctypes.POINTER(f32)]
+        L.ref_quantize_value.restype = ctypes.c_int16
+        L.ref_quantize_value.argtypes = [f32, u8]
+        L.ref_category.restype = i32
+        L.ref_category.argtypes = [i32]
+        L.ref_category_pattern.restype = u16
+        L.ref_category_pattern.argtypes = [i32, i32]
+        L.ref_package_merge.restype = i32
+        L.ref_package_merge.argtypes = [ctypes.POINTER(ctypes.c_uint64), i32, i32, ctypes.POINTER(i32)]
+        L.ref_code_lengths.restype = i32
+        L.ref_code_lengths.argtypes = [ctypes.POINTER(ctypes.c_uint64), i32, ctypes.POINTER(u8), ctypes.POINTER(i32)]
+        L.ref_assign_codes.argtypes = [ctypes.POINTER(u8), ctypes.POINTER(i32), i32, ctypes.POINTER(u16), ctypes.POINTER(u8)]
+        L.ref_subsample_resort.argtypes = [ctypes.POINTER(f32), i32, i32, i32, i32, i32, ctypes.POINTER(f32)]
+        L.ref_forward.restype = i32
+        L.ref_forward.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+        L.ref_encode_coefficients.restype = i32
+        L.ref_encode_coefficients.argtypes = [vp, ctypes.c_size_t, i32, i32, ctypes.POINTER(RefOptions), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+        L.ref_encode.restype = i32
+        L.ref_encode.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+        L.ref_encode_mt.restype = i32
+        L.ref_encode_mt.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), i32, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+        L.ref_free.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with code {code}")
+        self.code = code
+
+
+def make_options(preset: int, luma_q, chroma_q, bits_per_channel: int = 8) -> RefOptions:
+    o = RefOptions()
+    o.preset = int(preset)
+    o.bits_per_channel = int(bits_per_channel)
+    for i in range(64):
+        o.luma_q[i] = int(luma_q[i])
+        o.chroma_q[i] = int(chroma_q[i])
+    return o
+
+
+def _as_u16_rgb(rgb) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(rgb), dtype=np.uint16)
+    if a.ndim != 3 or a.shape[2] != 3:
+        raise ValueError("rgb must be HxWx3")
+    return a
+
+
+def encode(rgb, maxval: int, preset: int, luma_q, chroma_q, bits_per_channel: int = 8, threads: int = 1) -> bytes:
+    """Whole reference encode path (JpegImageWriter::write_image, jpeg.rs:64-75)."""
+    a = _as_u16_rgb(rgb)
+    h, w, _ = a.shape
+    opt = make_options(preset, luma_q, chroma_q, bits_per_channel)
+    out = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    L = lib()
+    if threads > 1:
+        rc = L.ref_encode_mt(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), int(threads), ctypes.byref(out), ctypes.byref(n))
+    else:
+        rc = L.ref_encode(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), ctypes.byref(out), ctypes.byref(n))
+    if rc != 0:
+        raise OracleError(rc, "ref_encode")
+    data = ctypes.string_at(out.value, n.value)
+    L.ref_free(out)
+    return data
+
+
+def forward(rgb, maxval: int, preset: int, luma_q, chroma_q) -> np.ndarray:
+    """Front half: quantised zigzag blocks in MCU emission order, shape (nblocks, 64) int16."""
+    a = _as_u16_rgb(rgb)
+    h, w, _ = a.shape
+    opt = make_options(preset, luma_q, chroma_q)
+    out = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    L = lib()
+    rc = L.ref_forward(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), ctypes.byref(out), ctypes.byref(n))
+    if rc != 0:
+        raise OracleError(rc, "ref_forward")
+    buf = ctypes.string_at(out.value, n.value * 128)
+    L.ref_free(out)
+    return np.frombuffer(buf, dtype=np.int16).reshape(n.value, 64).copy()
+
+
+def encode_coefficients(coef_zz: np.ndarray, width: int, height: int, preset: int, luma_q, chroma_q,
+                        bits_per_channel: int = 8) -> bytes:
+    """Back half: emission-order zigzag blocks -> complete JPEG file."""
+    c = np.ascontiguousarray(coef_zz, dtype=np.int16)
+    opt = make_options(preset, luma_q, chroma_q, bits_per_channel)
+    out = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    L = lib()
+    rc = L.ref_encode_coefficients(c.ctypes.data, c.shape[0], int(width), int(height), ctypes.byref(opt),
+                                   ctypes.byref(out), ctypes.byref(n))
+    if rc != 0:
+        raise OracleError(rc, "ref_encode_coefficients")
+    data = ctypes.string_at(out.value, n.value)
+    L.ref_free(out)
+    return data
+
+
+def package_merge(sorted_freq, limit: int):
+    L = lib()
+    n = len(sorted_freq)
+    f = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in sorted_freq])
+    out = (ctypes.c_int * max(n, 1))()
+    rc = L.ref_package_merge(f, n, int(limit), out)
+    if rc != 0:
+        raise OracleError(rc, "ref_package_merge")
+    return [out[i] for i in range(n)]
+
+
+def code_lengths(hist):
+    """(symbols in ascending-frequency order, lengths incl. the +1) for a 256-bin histogram."""
+    L = lib()
+    h = (ctypes.c_uint64 * 256)(*[int(x) for x in hist])
+    syms = (ctypes.c_uint8 * 256)()
+    lens = (ctypes.c_int * 256)()
+    n = L.ref_code_lengths(h, 256, syms, lens)
+    if n < 0:
+        raise OracleError(n, "ref_code_lengths")
+    return [syms[i] for i in range(n)], [lens[i] for i in range(n)]
+
+
+def assign_codes(symbols, lengths):
+    L = lib()
+    n = len(symbols)
+    s = (ctypes.c_uint8 * 256)(*symbols)
+    ln = (ctypes.c_int * 256)(*lengths)
+    code = (ctypes.c_uint16 * 256)()
+    clen = (ctypes.c_uint8 * 256)()
+    L.ref_assign_codes(s, ln, n, code, clen)
+    return {symbols[i]: (code[symbols[i]], clen[symbols[i]]) for i in range(n)}
+
+
+def fast_arai(values, stride: int = 1) -> np.ndarray:
+    a = np.ascontiguousarray(values, dtype=np.float32).copy()
+    lib().ref_fast_arai(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(stride))
+    return a
+
+
+def dct_block(block) -> np.ndarray:
+    a = np.ascontiguousarray(block, dtype=np.float32).reshape(64).copy()
+    lib().ref_dct_block(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return a
+
+
+def rgb_to_ycbcr(r: float, g: float, b: float):
+    out = (ctypes.c_float * 3)()
+    lib().ref_rgb_to_ycbcr(r, g, b, out)
+    return out[0], out[1], out[2]
+
+
+def normalize(value: int, maxval: int) -> float:
+    return lib().ref_normalize(int(value), int(maxval))
+
+
+def quantize_value(d: float, q: int) -> int:
+    return lib().ref_quantize_value(float(d), int(q))
+
+
+def category(v: int) -> int:
+    return lib().ref_category(int(v))
+
+
+def category_pattern(v: int, cat: int) -> int:
+    return lib().ref_category_pattern(int(v), int(cat))
+
+
+def subsample_resort(plane: np.ndarray, hr: int, vr: int, average: bool) -> np.ndarray:
+    p = np.ascontiguousarray(plane, dtype=np.float32)
+    h, w = p.shape
+    out = np.zeros((h // vr) * (w // hr), dtype=np.float32)
+    lib().ref_subsample_resort(p.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), w, h, hr, vr, int(average),
+                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return out
