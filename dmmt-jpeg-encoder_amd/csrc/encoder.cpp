@@ -1,0 +1,663 @@
+// encoder.cpp -- context, device workspace and the C ABI of include/dmmt_jpeg.h.
+//
+// The host only orchestrates: it validates arguments, sizes the pooled device
+// workspace, uploads the (tiny) quantisation and normalisation tables and
+// enqueues the kernels of kernels.hip.  Every byte of the JPEG (headers
+// included) is produced on the GPU; there is no CPU fallback -- without a
+// gfx950 device dmmt_ctx_create fails with DMMT_E_NO_DEVICE.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/dmmt_jpeg.h"
+#include "jpeg_common.hpp"
+#include "kernels.hpp"
+
+using namespace dmmt;
+
+namespace {
+
+const char* kStageNames[ST_COUNT] = {"front",       "dcdiff",     "tables",      "bits",
+                                     "scan",        "pack",       "stuff_count", "stuff_scan",
+                                     "stuff_write", "ac_hist"};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct EventPair {
+    int stage;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct dmmt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // workspace (grown on demand, never shrunk)
+    DevBuf coef, dc, dcdiff, block_bits, chunk_bits, chunk_off, ac_hist, dc_hist, code_tab, hdr_len, total_bits,
+        packed, seg_ff, status, lut, qtab, qtab_u8;
+    // host-API staging
+    DevBuf in, out, out_len, dct;
+    // uploaded table state
+    int lut_maxval = -1, lut_sb = -1;
+    uint8_t q_cached[128];
+    bool q_valid = false;
+    // profiling
+    bool profile = false;
+    std::vector<EventPair> pending;
+    std::vector<hipEvent_t> free_events;
+    double stage_ms[ST_COUNT] = {0};
+    int stage_launches[ST_COUNT] = {0};
+};
+
+namespace {
+
+int hip_err(hipError_t e) {
+    if (e == hipSuccess) return DMMT_OK;
+    if (e == hipErrorOutOfMemory) return DMMT_E_OUT_OF_MEMORY;
+    return DMMT_E_HIP;
+}
+
+#define HIP_TRY(expr)                      \
+    do {                                   \
+        hipError_t e_ = (expr);            \
+        if (e_ != hipSuccess) return hip_err(e_); \
+    } while (0)
+
+// grow a device buffer; zero-fill new memory when `zero`
+int ensure(DevBuf& b, size_t bytes, bool zero = false) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return DMMT_OK;
+    if (b.p) HIP_TRY(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    HIP_TRY(hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+    if (zero) HIP_TRY(hipMemset(b.p, 0, bytes));
+    return DMMT_OK;
+}
+
+void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+int validate(const dmmt_options* opt) {
+    if (!opt) return DMMT_E_INVALID_ARGUMENT;
+    if (opt->subsampling < 0 || opt->subsampling > 2) return DMMT_E_INVALID_ARGUMENT;
+    if (opt->bits_per_channel < 0 || opt->bits_per_channel > 255) return DMMT_E_INVALID_ARGUMENT;
+    for (int i = 0; i < 64; ++i)
+        if (opt->luma_q[i] == 0 || opt->chroma_q[i] == 0) return DMMT_E_INVALID_ARGUMENT;
+    if (opt->restart_interval != 0) return DMMT_E_INVALID_ARGUMENT;  // extension not enabled yet
+    return DMMT_OK;
+}
+
+int make_checked_geom(int w, int h, int sub, int maxval, int ri, Geom* g) {
+    if (w <= 0 || h <= 0) return DMMT_E_INVALID_ARGUMENT;  // the reference panics on an empty image
+    *g = make_geom(w, h, sub, maxval, ri);
+    if (g->wp > 65535 || g->hp > 65535) return DMMT_E_INVALID_ARGUMENT;  // u16 padded size
+    return DMMT_OK;
+}
+
+// Upload quantisation tables (f32 for the quantiser, u8 for DQT) and the
+// `v as f32 / max as f32` table (color.rs:45-53; host f32 division is IEEE
+// correctly rounded, identical to the reference's).
+int upload_tables(dmmt_ctx* c, const dmmt_options* opt, int maxval, int sb, hipStream_t st) {
+    int rc;
+    if ((rc = ensure(c->qtab, 128 * sizeof(float)))) return rc;
+    if ((rc = ensure(c->qtab_u8, 128))) return rc;
+    uint8_t q[128];
+    memcpy(q, opt->luma_q, 64);
+    memcpy(q + 64, opt->chroma_q, 64);
+    if (!c->q_valid || memcmp(q, c->q_cached, 128) != 0) {
+        float qf[128];
+        for (int i = 0; i < 128; ++i) qf[i] = (float)q[i];
+        HIP_TRY(hipMemcpyAsync(c->qtab.p, qf, sizeof qf, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(c->qtab_u8.p, q, 128, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        memcpy(c->q_cached, q, 128);
+        c->q_valid = true;
+    }
+    if (c->lut_maxval != maxval || c->lut_sb != sb) {
+        const size_t n = sb == 1 ? 256 : 65536;
+        if ((rc = ensure(c->lut, n * sizeof(float)))) return rc;
+        std::vector<float> lut(n);
+        for (size_t v = 0; v < n; ++v) lut[v] = (float)v / (float)maxval;
+        HIP_TRY(hipMemcpyAsync(c->lut.p, lut.data(), n * sizeof(float), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        c->lut_maxval = maxval;
+        c->lut_sb = sb;
+    }
+    return DMMT_OK;
+}
+
+int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
+    int rc;
+    const size_t nb = (size_t)g.bpf * nf;
+    const size_t nch = (size_t)g.nch * nf;
+    if ((rc = ensure(c->coef, nb * 64 * sizeof(int16_t)))) return rc;
+    if ((rc = ensure(c->dc, nb * sizeof(int16_t)))) return rc;
+    if ((rc = ensure(c->dcdiff, nb * sizeof(int16_t)))) return rc;
+    if ((rc = ensure(c->block_bits, nb * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c->chunk_bits, nch * 8))) return rc;
+    if ((rc = ensure(c->chunk_off, nch * 8))) return rc;
+    if ((rc = ensure(c->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
+    if ((rc = ensure(c->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
+    if ((rc = ensure(c->code_tab, (size_t)nf * 1024 * 4))) return rc;
+    if ((rc = ensure(c->hdr_len, (size_t)nf * 4))) return rc;
+    if ((rc = ensure(c->total_bits, (size_t)nf * 8))) return rc;
+    if ((rc = ensure(c->packed, (size_t)nf * (size_t)g.packed_words * 4))) return rc;
+    if ((rc = ensure(c->seg_ff, (size_t)nf * (size_t)g.nseg_cap * 4))) return rc;
+    if ((rc = ensure(c->status, 16, true))) return rc;
+    w->coef = (int16_t*)c->coef.p;
+    w->dc = (int16_t*)c->dc.p;
+    w->dcdiff = (int16_t*)c->dcdiff.p;
+    w->block_bits = (uint32_t*)c->block_bits.p;
+    w->chunk_bits = (unsigned long long*)c->chunk_bits.p;
+    w->chunk_off = (unsigned long long*)c->chunk_off.p;
+    w->ac_hist = (uint32_t*)c->ac_hist.p;
+    w->dc_hist = (uint32_t*)c->dc_hist.p;
+    w->code_tab = (uint32_t*)c->code_tab.p;
+    w->hdr_len = (uint32_t*)c->hdr_len.p;
+    w->total_bits = (unsigned long long*)c->total_bits.p;
+    w->packed = (uint32_t*)c->packed.p;
+    w->seg_ff = (uint32_t*)c->seg_ff.p;
+    w->status = (int*)c->status.p;
+    w->norm_lut = (const float*)c->lut.p;
+    w->qtab = (const float*)c->qtab.p;
+    w->qtab_u8 = (const uint8_t*)c->qtab_u8.p;
+    return DMMT_OK;
+}
+
+hipEvent_t take_event(dmmt_ctx* c) {
+    if (!c->free_events.empty()) {
+        hipEvent_t e = c->free_events.back();
+        c->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// fold completed event pairs into the per-stage totals
+void drain_events(dmmt_ctx* c) {
+    for (auto& p : c->pending) {
+        (void)hipEventSynchronize(p.b);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->stage_ms[p.stage] += ms;
+            c->stage_launches[p.stage] += 1;
+        }
+        c->free_events.push_back(p.a);
+        c->free_events.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+struct StageTimer {
+    dmmt_ctx* c;
+    int stage;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    StageTimer(dmmt_ctx* c_, int s, hipStream_t st_) : c(c_), stage(s), st(st_) {
+        if (c->profile) {
+            a = take_event(c);
+            b = take_event(c);
+            if (a) (void)hipEventRecord(a, st);
+        }
+    }
+    ~StageTimer() {
+        if (a && b) {
+            (void)hipEventRecord(b, st);
+            c->pending.push_back({stage, a, b});
+            if (c->pending.size() > 4096) drain_events(c);
+        }
+    }
+};
+
+// Enqueue the entropy back half (k_dcdiff .. k_stuff_write) for coefficients
+// already in w.coef / w.dc with AC histograms accumulated.
+int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bits, uint8_t* out, size_t out_stride,
+                      uint32_t* out_len, hipStream_t st) {
+    const Stage order[] = {ST_DCDIFF, ST_TABLES, ST_BITS, ST_SCAN, ST_PACK, ST_STUFF_COUNT, ST_STUFF_SCAN,
+                           ST_STUFF_WRITE};
+    for (Stage s : order) {
+        StageTimer t(c, s, st);
+        HIP_TRY(launch_stage(s, nf, g, w, bits, out, out_stride, out_len, st));
+    }
+    return DMMT_OK;
+}
+
+int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, int nf, const Geom& g,
+                   const dmmt_options* opt, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st) {
+    Work w;
+    int rc;
+    if ((rc = ensure_work(c, g, nf, &w))) return rc;
+    if ((rc = upload_tables(c, opt, g.maxval, sb, st))) return rc;
+    w.norm_lut = (const float*)c->lut.p;
+    {
+        StageTimer t(c, ST_FRONT, st);
+        HIP_TRY(launch_front(d_rgb, frame_stride, sb, nf, g, w, st));
+    }
+    return enqueue_back_half(c, g, nf, w, opt->bits_per_channel, out, out_stride, out_len, st);
+}
+
+// read and clear the device status word
+int take_status(dmmt_ctx* c, hipStream_t st) {
+    if (!c->status.p) return DMMT_OK;
+    int s = 0;
+    HIP_TRY(hipMemcpyAsync(&s, c->status.p, sizeof s, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (s) HIP_TRY(hipMemsetAsync(c->status.p, 0, sizeof(int), st));
+    if (s & 1) return DMMT_E_VALUE_EXCEEDS_MAX;
+    if (s & 2) return DMMT_E_HUFFMAN_SYMBOL_MISSING;
+    return DMMT_OK;
+}
+
+int set_device(dmmt_ctx* c) { return hip_err(hipSetDevice(c->device)); }
+
+}  // namespace
+
+// ===================================================================== C ABI
+
+extern "C" int dmmt_device_count(int* count) {
+    if (!count) return DMMT_E_INVALID_ARGUMENT;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
+    if (!out) return DMMT_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return DMMT_E_NO_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return DMMT_E_NO_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DMMT_E_NO_DEVICE;  // code objects are gfx950 only
+    if (hipSetDevice(device) != hipSuccess) return DMMT_E_NO_DEVICE;
+    dmmt_ctx* c = new dmmt_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return DMMT_E_HIP;
+    }
+    *out = c;
+    return DMMT_OK;
+}
+
+extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    drain_events(c);
+    for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
+    DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff, &c->block_bits, &c->chunk_bits, &c->chunk_off,
+                      &c->ac_hist,    &c->dc_hist,    &c->code_tab, &c->hdr_len,  &c->total_bits, &c->packed,
+                      &c->seg_ff,     &c->status,     &c->lut,    &c->qtab,       &c->qtab_u8,    &c->in,
+                      &c->out,        &c->out_len,    &c->dct};
+    for (DevBuf* b : bufs) release(*b);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" int dmmt_ctx_synchronize(dmmt_ctx* c) {
+    if (!c) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    return take_status(c, c->stream);
+}
+
+extern "C" size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t subsampling) {
+    if (subsampling < 0 || subsampling > 2 || width == 0 || height == 0) return 0;
+    Geom g = make_geom(width, height, subsampling, 255, 0);
+    return max_jpeg_bytes(g);
+}
+
+extern "C" int dmmt_encode_device(dmmt_ctx* c, const dmmt_device_frames* f, const dmmt_options* opt, void* stream) {
+    if (!c || !f) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = validate(opt))) return rc;
+    if (f->n_frames <= 0 || !f->d_rgb || !f->d_out || !f->d_out_len) return DMMT_E_INVALID_ARGUMENT;
+    if (f->sample_bytes != 1 && f->sample_bytes != 2) return DMMT_E_INVALID_ARGUMENT;
+    Geom g;
+    if ((rc = make_checked_geom(f->width, f->height, opt->subsampling, f->maxval, opt->restart_interval, &g))) return rc;
+    if (f->out_stride < max_jpeg_bytes(g)) return DMMT_E_CAPACITY;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return enqueue_encode(c, f->d_rgb, f->frame_stride, f->sample_bytes, f->n_frames, g, opt, f->d_out, f->out_stride,
+                          f->d_out_len, st);
+}
+
+// Host-memory batch of equal-geometry images -> host JPEGs.
+static int encode_host_group(dmmt_ctx* c, const dmmt_image* imgs, int n, const dmmt_options* opt, uint8_t** outs,
+                             size_t* lens) {
+    const dmmt_image& i0 = imgs[0];
+    Geom g;
+    int rc;
+    if ((rc = make_checked_geom(i0.width, i0.height, opt->subsampling, i0.maxval, opt->restart_interval, &g))) return rc;
+    const size_t frame_bytes = (size_t)i0.width * i0.height * 3 * i0.sample_bytes;
+    const size_t stride = (frame_bytes + 255) / 256 * 256;
+    const size_t out_stride = (max_jpeg_bytes(g) + 255) / 256 * 256;
+    if ((rc = ensure(c->in, stride * n))) return rc;
+    if ((rc = ensure(c->out, out_stride * n))) return rc;
+    if ((rc = ensure(c->out_len, sizeof(uint32_t) * n))) return rc;
+    hipStream_t st = c->stream;
+    for (int i = 0; i < n; ++i)
+        HIP_TRY(hipMemcpyAsync((uint8_t*)c->in.p + stride * i, imgs[i].rgb, frame_bytes, hipMemcpyHostToDevice, st));
+    if ((rc = enqueue_encode(c, c->in.p, stride, i0.sample_bytes, n, g, opt, (uint8_t*)c->out.p, out_stride,
+                             (uint32_t*)c->out_len.p, st)))
+        return rc;
+    std::vector<uint32_t> L(n);
+    HIP_TRY(hipMemcpyAsync(L.data(), c->out_len.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = take_status(c, st))) return rc;
+    for (int i = 0; i < n; ++i) {
+        if (L[i] == 0 || L[i] > out_stride) return DMMT_E_CAPACITY;
+        uint8_t* h = (uint8_t*)malloc(L[i]);
+        if (!h) return DMMT_E_OUT_OF_MEMORY;
+        HIP_TRY(hipMemcpyAsync(h, (uint8_t*)c->out.p + out_stride * i, L[i], hipMemcpyDeviceToHost, st));
+        outs[i] = h;
+        lens[i] = L[i];
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return DMMT_OK;
+}
+
+static int check_image(const dmmt_image* img) {
+    if (!img || !img->rgb) return DMMT_E_INVALID_ARGUMENT;
+    if (img->sample_bytes != 1 && img->sample_bytes != 2) return DMMT_E_INVALID_ARGUMENT;
+    if (img->width == 0 || img->height == 0) return DMMT_E_INVALID_ARGUMENT;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_jpeg_encode_batch(dmmt_ctx* c, const dmmt_image* imgs, int n, const dmmt_options* opt,
+                                      uint8_t** outs, size_t* lens) {
+    if (!c || !imgs || n <= 0 || !outs || !lens) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = validate(opt))) return rc;
+    for (int i = 0; i < n; ++i) {
+        if ((rc = check_image(&imgs[i]))) return rc;
+        outs[i] = nullptr;
+        lens[i] = 0;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    int i = 0;
+    while (i < n) {  // runs of equal geometry share launches
+        int j = i + 1;
+        while (j < n && imgs[j].width == imgs[i].width && imgs[j].height == imgs[i].height &&
+               imgs[j].maxval == imgs[i].maxval && imgs[j].sample_bytes == imgs[i].sample_bytes)
+            ++j;
+        if ((rc = encode_host_group(c, imgs + i, j - i, opt, outs + i, lens + i))) {
+            for (int k = 0; k < n; ++k) {
+                free(outs[k]);
+                outs[k] = nullptr;
+                lens[k] = 0;
+            }
+            return rc;
+        }
+        i = j;
+    }
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_jpeg_encode(dmmt_ctx* c, const dmmt_image* img, const dmmt_options* opt, uint8_t** out,
+                                size_t* out_len) {
+    if (!out || !out_len) return DMMT_E_INVALID_ARGUMENT;
+    return dmmt_jpeg_encode_batch(c, img, 1, opt, out, out_len);
+}
+
+extern "C" int dmmt_forward_blocks(dmmt_ctx* c, const dmmt_image* img, const dmmt_options* opt, int16_t* coef,
+                                   size_t cap_blocks, size_t* nblocks) {
+    if (!c || !coef || !nblocks) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = validate(opt)) || (rc = check_image(img))) return rc;
+    Geom g;
+    if ((rc = make_checked_geom(img->width, img->height, opt->subsampling, img->maxval, 0, &g))) return rc;
+    *nblocks = (size_t)g.bpf;
+    if (cap_blocks < (size_t)g.bpf) return DMMT_E_CAPACITY;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    hipStream_t st = c->stream;
+    const size_t frame_bytes = (size_t)img->width * img->height * 3 * img->sample_bytes;
+    Work w;
+    if ((rc = ensure(c->in, frame_bytes))) return rc;
+    if ((rc = ensure_work(c, g, 1, &w))) return rc;
+    if ((rc = upload_tables(c, opt, g.maxval, img->sample_bytes, st))) return rc;
+    w.norm_lut = (const float*)c->lut.p;
+    HIP_TRY(hipMemcpyAsync(c->in.p, img->rgb, frame_bytes, hipMemcpyHostToDevice, st));
+    {
+        StageTimer t(c, ST_FRONT, st);
+        HIP_TRY(launch_front(c->in.p, frame_bytes, img->sample_bytes, 1, g, w, st));
+    }
+    HIP_TRY(hipMemcpyAsync(coef, w.coef, (size_t)g.bpf * 128, hipMemcpyDeviceToHost, st));
+    // the histograms of this partial run are not consumed: clear them
+    HIP_TRY(hipMemsetAsync(w.ac_hist, 0, (size_t)kHistReps * 512 * 4, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return take_status(c, st);
+}
+
+extern "C" int dmmt_encode_coefficients(dmmt_ctx* c, const int16_t* coef, size_t nblocks, uint16_t width,
+                                        uint16_t height, const dmmt_options* opt, uint8_t** out, size_t* out_len) {
+    if (!c || !coef || !out || !out_len) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = validate(opt))) return rc;
+    Geom g;
+    if ((rc = make_checked_geom(width, height, opt->subsampling, 255, 0, &g))) return rc;
+    if (nblocks != (size_t)g.bpf) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    hipStream_t st = c->stream;
+    Work w;
+    if ((rc = ensure_work(c, g, 1, &w))) return rc;
+    if ((rc = upload_tables(c, opt, 255, 1, st))) return rc;
+    const size_t out_stride = max_jpeg_bytes(g);
+    if ((rc = ensure(c->out, out_stride))) return rc;
+    if ((rc = ensure(c->out_len, 4))) return rc;
+    HIP_TRY(hipMemcpyAsync(w.coef, coef, nblocks * 128, hipMemcpyHostToDevice, st));
+    {
+        StageTimer t(c, ST_AC_HIST, st);
+        HIP_TRY(launch_ac_hist(1, g, w, st));
+    }
+    if ((rc = enqueue_back_half(c, g, 1, w, opt->bits_per_channel, (uint8_t*)c->out.p, out_stride,
+                                (uint32_t*)c->out_len.p, st)))
+        return rc;
+    uint32_t L = 0;
+    HIP_TRY(hipMemcpyAsync(&L, c->out_len.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = take_status(c, st))) return rc;
+    if (L == 0 || L > out_stride) return DMMT_E_CAPACITY;
+    uint8_t* h = (uint8_t*)malloc(L);
+    if (!h) return DMMT_E_OUT_OF_MEMORY;
+    HIP_TRY(hipMemcpy(h, c->out.p, L, hipMemcpyDeviceToHost));
+    *out = h;
+    *out_len = L;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_dct_transform(dmmt_ctx* c, float* blocks, size_t len) {
+    if (!c || (!blocks && len) || len % 64) return DMMT_E_INVALID_ARGUMENT;
+    if (len == 0) return DMMT_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if ((rc = ensure(c->dct, len * sizeof(float)))) return rc;
+    hipStream_t st = c->stream;
+    HIP_TRY(hipMemcpyAsync(c->dct.p, blocks, len * sizeof(float), hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_dct_blocks((float*)c->dct.p, (long long)(len / 64), st));
+    HIP_TRY(hipMemcpyAsync(blocks, c->dct.p, len * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_convert_ppm_to_jpeg(dmmt_ctx* c, const char* input_path, const char* output_path,
+                                        const dmmt_options* opt) {
+    // lib.rs:59-77: open input, open output, read PPM, encode, write
+    if (!c || !input_path || !output_path) return DMMT_E_INVALID_ARGUMENT;
+    FILE* probe = fopen(input_path, "rb");
+    if (!probe) return DMMT_E_OPEN_INPUT;
+    fclose(probe);
+    FILE* fo = fopen(output_path, "wb");
+    if (!fo) return DMMT_E_OPEN_OUTPUT;
+    dmmt_image img;
+    int rc = dmmt_read_ppm(input_path, &img);
+    if (rc) {
+        fclose(fo);
+        return rc;
+    }
+    uint8_t* jpg = nullptr;
+    size_t n = 0;
+    rc = dmmt_jpeg_encode(c, &img, opt, &jpg, &n);
+    free((void*)img.rgb);
+    if (rc == DMMT_OK && fwrite(jpg, 1, n, fo) != n) rc = DMMT_E_WRITE_IMAGE_DATA;
+    free(jpg);
+    if (fclose(fo) != 0 && rc == DMMT_OK) rc = DMMT_E_WRITE_END_OF_FILE;
+    return rc;
+}
+
+extern "C" void dmmt_free(void* p) { free(p); }
+
+extern "C" const char* dmmt_error_name(int code) {
+    switch (code) {
+    case DMMT_OK: return "Ok";
+    case DMMT_E_PPM_MISSING_TOKEN: return "PPMFileDoesNotContainRequiredToken";
+    case DMMT_E_PPM_PARSE_TOKEN: return "ParsingOfTokenFailed";
+    case DMMT_E_PPM_INCOMPLETE_PIXEL: return "IncompletePixelParsed";
+    case DMMT_E_PPM_SIZE_MISMATCH: return "MismatchOfSizeBetweenHeaderAndValues";
+    case DMMT_E_INPUT_NOT_FOUND: return "InputFileNotFound";
+    case DMMT_E_NO_READ_PERMISSION: return "NoReadPermissionForInputFile";
+    case DMMT_E_OPEN_INPUT: return "UnableToOpenInputFileForReading";
+    case DMMT_E_OPEN_OUTPUT: return "UnableToOpenOutputFileForWriting";
+    case DMMT_E_WRITE_START_OF_FILE: return "FailedToWriteStartOfFile";
+    case DMMT_E_WRITE_HUFFMAN_TABLES: return "FailedToWriteHuffmanTables";
+    case DMMT_E_WRITE_END_OF_FILE: return "FailedToWriteEndOfFile";
+    case DMMT_E_WRITE_JFIF: return "FailedToWriteJfifApplicationHeader";
+    case DMMT_E_WRITE_QUANTIZATION_TABLE: return "FailedToWriteQuantizationTable";
+    case DMMT_E_WRITE_START_OF_FRAME: return "FailedToWriteStartOfFrame";
+    case DMMT_E_WRITE_START_OF_SCAN: return "FailedToWriteStartOfScan";
+    case DMMT_E_WRITE_IMAGE_DATA: return "FailedToWriteImageData";
+    case DMMT_E_HUFFMAN_SYMBOL_MISSING: return "HuffmanSymbolNotPresentInTranslator";
+    case DMMT_E_WRITE_BLOCK: return "FailedToWriteBlock";
+    case DMMT_E_VALUE_EXCEEDS_MAX: return "ValueExceedsMax";
+    case DMMT_E_CATEGORY_RANGE: return "CategoryOutOfRange";
+    case DMMT_E_INVALID_ARGUMENT: return "InvalidArgument";
+    case DMMT_E_HIP: return "HipError";
+    case DMMT_E_OUT_OF_MEMORY: return "OutOfMemory";
+    case DMMT_E_NO_DEVICE: return "NoDevice";
+    case DMMT_E_CAPACITY: return "Capacity";
+    default: return "Unknown";
+    }
+}
+
+extern "C" const char* dmmt_strerror(int code) {
+    switch (code) {
+    case DMMT_OK: return "ok";
+    case DMMT_E_PPM_MISSING_TOKEN: return "Expected token not found in PPM file";
+    case DMMT_E_PPM_PARSE_TOKEN: return "Parsing of PPM token failed";
+    case DMMT_E_PPM_INCOMPLETE_PIXEL: return "Incomplete pixel parsed";
+    case DMMT_E_PPM_SIZE_MISMATCH: return "The size in the header does not match the number of values";
+    case DMMT_E_INPUT_NOT_FOUND: return "Input file not found";
+    case DMMT_E_NO_READ_PERMISSION: return "No read permission for input file";
+    case DMMT_E_OPEN_INPUT: return "Unable to open input file for reading";
+    case DMMT_E_OPEN_OUTPUT: return "Unable to open output file for writing";
+    case DMMT_E_WRITE_IMAGE_DATA: return "Failed to write image data";
+    case DMMT_E_WRITE_END_OF_FILE: return "Failed to write end of file";
+    case DMMT_E_HUFFMAN_SYMBOL_MISSING: return "Huffman symbol not present in translator";
+    case DMMT_E_VALUE_EXCEEDS_MAX: return "Color value must not be greater than max value";
+    case DMMT_E_CATEGORY_RANGE: return "Value out of range for categorisation";
+    case DMMT_E_INVALID_ARGUMENT: return "Invalid argument";
+    case DMMT_E_HIP: return "HIP runtime error";
+    case DMMT_E_OUT_OF_MEMORY: return "Out of device memory";
+    case DMMT_E_NO_DEVICE: return "No gfx950 (MI355X) device available; this library has no CPU fallback";
+    case DMMT_E_CAPACITY: return "Output buffer too small";
+    default: return dmmt_error_name(code);
+    }
+}
+
+extern "C" int dmmt_ctx_set_profiling(dmmt_ctx* c, int enable) {
+    if (!c) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    drain_events(c);
+    c->profile = enable != 0;
+    for (int i = 0; i < ST_COUNT; ++i) {
+        c->stage_ms[i] = 0;
+        c->stage_launches[i] = 0;
+    }
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_ctx_profile(dmmt_ctx* c, double* ms, int32_t* launches, int n_stages) {
+    if (!c) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    (void)hipSetDevice(c->device);
+    drain_events(c);
+    for (int i = 0; i < n_stages && i < ST_COUNT; ++i) {
+        if (ms) ms[i] = c->stage_ms[i];
+        if (launches) launches[i] = c->stage_launches[i];
+    }
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_num_stages(void) { return ST_COUNT; }
+extern "C" const char* dmmt_stage_name(int s) { return s >= 0 && s < ST_COUNT ? kStageNames[s] : ""; }
+
+extern "C" int dmmt_device_malloc(dmmt_ctx* c, size_t bytes, void** ptr) {
+    if (!c || !ptr) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIP_TRY(hipMalloc(ptr, bytes ? bytes : 16));
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_device_free(dmmt_ctx* c, void* ptr) {
+    if (!c) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIP_TRY(hipFree(ptr));
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_memcpy_h2d(dmmt_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_memcpy_d2h(dmmt_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!c) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_fill_synthetic(dmmt_ctx* c, void* d_rgb, uint16_t width, uint16_t height, int32_t n_frames,
+                                   int32_t first_frame, uint32_t seed) {
+    if (!c || !d_rgb || n_frames <= 0) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIP_TRY(launch_synthetic((uint8_t*)d_rgb, width, height, n_frames, first_frame, seed, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DMMT_OK;
+}
+
+extern "C" const char* dmmt_build_info(void) {
+    return "dmmt-jpeg-encoder_amd: HIP kernels for gfx950, -ffp-contract=off, ABI " "1";
+}

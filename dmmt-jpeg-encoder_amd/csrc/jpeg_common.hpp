@@ -1,0 +1,71 @@
+// jpeg_common.hpp -- constants and geometry shared by host and device code.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dmmt {
+
+// frequency_block.rs:1-5: natural index of zigzag position i
+static constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// Histogram replicas per frame: the front/DC kernels add their per-workgroup
+// histograms into replica (blockIdx.x % kHistReps) to spread atomic traffic.
+static constexpr int kHistReps = 16;
+// Blocks per entropy chunk (bit-count / pack kernels): one workgroup each.
+static constexpr int kChunkBlocks = 128;
+// Worst-case entropy-coded bits of one block: DC code 16 + 12 extra bits, 63 AC
+// tokens of code 16 + 12 extra bits (|coef| <= 2048 for 8-bit-range input).
+static constexpr int kMaxBlockBits = 28 * 64;
+// Bytes per segment of the byte-stuffing pass.
+static constexpr int kStuffSeg = 4096;
+// Upper bound of the header the table kernel writes (SOI..SOS incl. DRI).
+static constexpr int kMaxHeaderBytes = 2 + 18 + 2 * 69 + 19 + 4 * (4 + 17 + 256) + 6 + 14;
+
+// Geometry of one frame (all frames of a launch share it).
+struct Geom {
+    int width, height;      // unpadded (SOF carries these, encoder.rs:231-240)
+    int wp, hp;             // padded to (8*hr, 8*vr) multiples (transformer.rs:48-51)
+    int hr, vr;             // chroma subsampling rates
+    int n_luma, bpm;        // Y blocks per MCU, blocks per MCU
+    int mcux, mcuy, nmcu;   // MCU grid
+    int maxval;             // PPM max value
+    int restart_interval;   // 0 = reference behaviour
+    long long bpf;          // blocks per frame
+    int nch;                // entropy chunks per frame
+    int nseg_cap;           // stuffing segments per frame (capacity)
+    long long packed_words; // words of the packed-bit buffer per frame
+};
+
+inline Geom make_geom(int width, int height, int subsampling, int maxval, int restart_interval) {
+    Geom g{};
+    g.width = width;
+    g.height = height;
+    g.hr = subsampling == 0 ? 1 : 2;
+    g.vr = subsampling == 2 ? 2 : 1;
+    g.wp = (width + 8 * g.hr - 1) / (8 * g.hr) * (8 * g.hr);
+    g.hp = (height + 8 * g.vr - 1) / (8 * g.vr) * (8 * g.vr);
+    g.n_luma = g.hr * g.vr;
+    g.bpm = g.n_luma + 2;
+    g.mcux = g.wp / (8 * g.hr);
+    g.mcuy = g.hp / (8 * g.vr);
+    g.nmcu = g.mcux * g.mcuy;
+    g.maxval = maxval;
+    g.restart_interval = restart_interval;
+    g.bpf = (long long)g.nmcu * g.bpm;
+    g.nch = (int)((g.bpf + kChunkBlocks - 1) / kChunkBlocks);
+    long long max_bits = g.bpf * kMaxBlockBits + 8LL * g.nmcu; // + restart padding
+    g.packed_words = (max_bits + 31) / 32 + 2;
+    long long max_bytes = g.packed_words * 4;
+    g.nseg_cap = (int)((max_bytes + kStuffSeg - 1) / kStuffSeg);
+    return g;
+}
+
+// Worst-case JPEG size: header + every scan byte stuffed + RST markers + EOI.
+inline size_t max_jpeg_bytes(const Geom& g) {
+    return (size_t)kMaxHeaderBytes + (size_t)g.packed_words * 4 * 2 + 2 * (size_t)g.nmcu + 2 + 64;
+}
+
+}  // namespace dmmt

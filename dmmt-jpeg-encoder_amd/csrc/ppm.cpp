@@ -1,0 +1,152 @@
+// ppm.cpp -- PPMImageReader (ppm.rs:19-252): ASCII P3 exactly as the reference
+// tokenises it, plus binary P6 (extension).  Host I/O, not part of the GPU path.
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/dmmt_jpeg.h"
+
+namespace {
+
+// Rust's char::is_ascii_whitespace: space, \t, \n, \x0C, \r (not \x0B)
+inline bool is_ws(uint8_t b) { return b == ' ' || b == '\t' || b == '\n' || b == 0x0C || b == '\r'; }
+
+// PPMTokenizer::next (ppm.rs:41-77).  A '#' comment runs to the next '\n',
+// which is consumed without ending the current token (ppm.rs:50-55).
+struct Tokenizer {
+    const uint8_t* p;
+    size_t n, i = 0;
+    bool next(std::string& tok) {
+        tok.clear();
+        bool in_comment = false;
+        while (i < n) {
+            const uint8_t b = p[i++];
+            if (in_comment) {
+                if (b == '\n') in_comment = false;
+                continue;
+            }
+            if (b == '#') {
+                in_comment = true;
+                continue;
+            }
+            if (is_ws(b)) {
+                if (!tok.empty()) break;
+            } else {
+                tok.push_back((char)b);
+            }
+        }
+        return !tok.empty();
+    }
+};
+
+// `str::parse::<u16>()`: optional '+', decimal digits, no overflow
+bool parse_u16(const std::string& t, uint16_t* out) {
+    size_t k = 0;
+    if (!t.empty() && t[0] == '+') k = 1;
+    if (k >= t.size()) return false;
+    uint32_t v = 0;
+    for (; k < t.size(); ++k) {
+        const char c = t[k];
+        if (c < '0' || c > '9') return false;
+        v = v * 10 + (uint32_t)(c - '0');
+        if (v > 65535) return false;
+    }
+    *out = (uint16_t)v;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) {
+    if (!img || (!data && len)) return DMMT_E_INVALID_ARGUMENT;
+    memset(img, 0, sizeof *img);
+    Tokenizer tz{data, len};
+    std::string tok;
+    // parse_header + check_header_version (ppm.rs:177-192)
+    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
+    const bool binary = tok == "P6";
+    if (tok != "P3" && !binary) return DMMT_E_PPM_MISSING_TOKEN;
+    uint16_t w, h, mx;
+    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
+    if (!parse_u16(tok, &w)) return DMMT_E_PPM_PARSE_TOKEN;
+    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
+    if (!parse_u16(tok, &h)) return DMMT_E_PPM_PARSE_TOKEN;
+    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
+    if (!parse_u16(tok, &mx)) return DMMT_E_PPM_PARSE_TOKEN;
+    const size_t npx = (size_t)w * h;
+    const int sb = mx > 255 ? 2 : 1;
+    uint8_t* buf = (uint8_t*)malloc(npx * 3 * (size_t)sb + 1);
+    if (!buf) return DMMT_E_OUT_OF_MEMORY;
+    if (binary) {
+        // P6: exactly one whitespace byte after maxval (already consumed by the
+        // tokenizer), then raw big-endian samples.
+        const size_t need = npx * 3 * (size_t)sb;
+        if (len - tz.i < need) {
+            free(buf);
+            return DMMT_E_PPM_SIZE_MISMATCH;
+        }
+        const uint8_t* s = data + tz.i;
+        if (sb == 1) {
+            memcpy(buf, s, need);
+        } else {
+            uint16_t* d = (uint16_t*)buf;
+            for (size_t k = 0; k < npx * 3; ++k) d[k] = (uint16_t)((s[2 * k] << 8) | s[2 * k + 1]);
+        }
+    } else {
+        // parse_all_dots (ppm.rs:224-252)
+        size_t count = 0;
+        bool over = false;
+        while (tz.next(tok)) {
+            uint16_t v;
+            if (!parse_u16(tok, &v)) {
+                free(buf);
+                return DMMT_E_PPM_PARSE_TOKEN;
+            }
+            if (count < npx * 3) {
+                if (sb == 1)
+                    buf[count] = (uint8_t)(v > 255 ? 255 : v);
+                else
+                    ((uint16_t*)buf)[count] = v;
+            }
+            if (v > mx) over = true;
+            ++count;
+        }
+        if (count % 3) {  // check_pixel_was_complete (ppm.rs:239-245)
+            free(buf);
+            return DMMT_E_PPM_INCOMPLETE_PIXEL;
+        }
+        if (count != npx * 3) {  // ppm.rs:165-175
+            free(buf);
+            return DMMT_E_PPM_SIZE_MISMATCH;
+        }
+        if (over) {  // RangeColorFormat::new panics (ppm.rs:155, color.rs:63-65)
+            free(buf);
+            return DMMT_E_VALUE_EXCEEDS_MAX;
+        }
+    }
+    img->width = w;
+    img->height = h;
+    img->maxval = mx;
+    img->sample_bytes = (uint16_t)sb;
+    img->rgb = buf;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_read_ppm(const char* path, dmmt_image* img) {
+    if (!path || !img) return DMMT_E_INVALID_ARGUMENT;
+    struct stat st;
+    if (stat(path, &st) != 0) return errno == EACCES ? DMMT_E_NO_READ_PERMISSION : DMMT_E_INPUT_NOT_FOUND;
+    FILE* f = fopen(path, "rb");
+    if (!f) return errno == EACCES ? DMMT_E_NO_READ_PERMISSION : DMMT_E_OPEN_INPUT;
+    std::vector<uint8_t> data;
+    data.resize((size_t)st.st_size);
+    const size_t got = st.st_size ? fread(data.data(), 1, data.size(), f) : 0;
+    fclose(f);
+    if (got != data.size()) return DMMT_E_OPEN_INPUT;
+    return dmmt_parse_ppm(data.data(), data.size(), img);
+}

@@ -1,0 +1,489 @@
+"""Python host mirror of the reference encoder API over the gfx950 C ABI.
+
+The reference (SilverlightningY/dmmt-jpeg-encoder) is a Rust crate whose public
+seam is ``JpegImageWriter::write_image`` (src/image/writer/jpeg.rs:64-75),
+reached from ``convert_ppm_to_jpeg`` (src/lib.rs:59-77).  This module mirrors
+those names, their argument meaning and their error behaviour, and calls
+``lib/libdmmt_jpeg.so`` (include/dmmt_jpeg.h) through ctypes.  All compute runs
+on the GPU; when the library or a gfx950 device is missing this module raises --
+it never falls back to a CPU path.
+
+One HIP runtime per process: torch wheels bundle their own libamdhip64.so.7.
+If torch is importable it is imported *before* the library is loaded so that
+both bind to the same runtime (loading ours first and torch afterwards would map
+two runtimes into one process).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import io
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdmmt_jpeg.so")
+CLI_PATH = os.path.join(_HERE, "bin", "dmmt-jpeg-encoder")
+
+try:  # see module docstring: bind the library to torch's HIP runtime if torch is present
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the product
+    torch = None
+
+_lib = None
+
+# ---------------------------------------------------------------- errors
+
+
+class Error(Exception):
+    """error::Error (src/error.rs:3-22) plus the states where the reference panics."""
+
+    def __init__(self, code: int, context: str = ""):
+        self.code = code
+        self.name = lib().dmmt_error_name(code).decode() if _lib is not None else str(code)
+        msg = lib().dmmt_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{self.name}: {msg}" + (f" ({context})" if context else ""))
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def build() -> str:
+    """Compile the HIP library and CLI in-tree (hipcc --offload-arch=gfx950)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "-j8"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LibraryMissing(f"{LIB_PATH} is not built; run build() or `make -C {_HERE}` -- there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i32, u16 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_uint16
+    P = ctypes.POINTER
+    L.dmmt_ctx_create.argtypes = [ctypes.c_int, P(vp)]
+    L.dmmt_ctx_destroy.argtypes = [vp]
+    L.dmmt_ctx_destroy.restype = None
+    L.dmmt_device_count.argtypes = [P(ctypes.c_int)]
+    L.dmmt_ctx_synchronize.argtypes = [vp]
+    L.dmmt_jpeg_encode.argtypes = [vp, P(DmmtImage), P(DmmtOptions), P(vp), P(sz)]
+    L.dmmt_jpeg_encode_batch.argtypes = [vp, P(DmmtImage), ctypes.c_int, P(DmmtOptions), P(vp), P(sz)]
+    L.dmmt_encode_device.argtypes = [vp, P(DmmtDeviceFrames), P(DmmtOptions), vp]
+    L.dmmt_max_jpeg_bytes.argtypes = [u16, u16, i32]
+    L.dmmt_max_jpeg_bytes.restype = sz
+    L.dmmt_forward_blocks.argtypes = [vp, P(DmmtImage), P(DmmtOptions), vp, sz, P(sz)]
+    L.dmmt_encode_coefficients.argtypes = [vp, vp, sz, u16, u16, P(DmmtOptions), P(vp), P(sz)]
+    L.dmmt_dct_transform.argtypes = [vp, vp, sz]
+    L.dmmt_quantization_preset.argtypes = [i32, vp, vp]
+    L.dmmt_quality_tables.argtypes = [i32, vp, vp]
+    L.dmmt_default_options.argtypes = [P(DmmtOptions)]
+    L.dmmt_default_options.restype = None
+    L.dmmt_read_ppm.argtypes = [ctypes.c_char_p, P(DmmtImage)]
+    L.dmmt_parse_ppm.argtypes = [vp, sz, P(DmmtImage)]
+    L.dmmt_convert_ppm_to_jpeg.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, P(DmmtOptions)]
+    L.dmmt_free.argtypes = [vp]
+    L.dmmt_free.restype = None
+    L.dmmt_strerror.argtypes = [ctypes.c_int]
+    L.dmmt_strerror.restype = ctypes.c_char_p
+    L.dmmt_error_name.argtypes = [ctypes.c_int]
+    L.dmmt_error_name.restype = ctypes.c_char_p
+    L.dmmt_ctx_set_profiling.argtypes = [vp, ctypes.c_int]
+    L.dmmt_ctx_profile.argtypes = [vp, P(ctypes.c_double), P(i32), ctypes.c_int]
+    L.dmmt_num_stages.argtypes = []
+    L.dmmt_stage_name.argtypes = [ctypes.c_int]
+    L.dmmt_stage_name.restype = ctypes.c_char_p
+    L.dmmt_device_malloc.argtypes = [vp, sz, P(vp)]
+    L.dmmt_device_free.argtypes = [vp, vp]
+    L.dmmt_memcpy_h2d.argtypes = [vp, vp, vp, sz]
+    L.dmmt_memcpy_d2h.argtypes = [vp, vp, vp, sz]
+    L.dmmt_fill_synthetic.argtypes = [vp, vp, u16, u16, i32, i32, ctypes.c_uint32]
+    L.dmmt_build_info.argtypes = []
+    L.dmmt_build_info.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+# ---------------------------------------------------------------- C structs
+
+class DmmtImage(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint16), ("height", ctypes.c_uint16), ("maxval", ctypes.c_uint16),
+                ("sample_bytes", ctypes.c_uint16), ("rgb", ctypes.c_void_p)]
+
+
+class DmmtOptions(ctypes.Structure):
+    _fields_ = [("subsampling", ctypes.c_int32), ("bits_per_channel", ctypes.c_int32),
+                ("luma_q", ctypes.c_uint8 * 64), ("chroma_q", ctypes.c_uint8 * 64),
+                ("n_threads", ctypes.c_int32), ("restart_interval", ctypes.c_int32)]
+
+
+class DmmtDeviceFrames(ctypes.Structure):
+    _fields_ = [("d_rgb", ctypes.c_void_p), ("frame_stride", ctypes.c_size_t), ("n_frames", ctypes.c_int32),
+                ("width", ctypes.c_uint16), ("height", ctypes.c_uint16), ("maxval", ctypes.c_uint16),
+                ("sample_bytes", ctypes.c_uint16), ("d_out", ctypes.c_void_p), ("out_stride", ctypes.c_size_t),
+                ("d_out_len", ctypes.c_void_p)]
+
+
+def _check(rc: int, what: str = ""):
+    if rc != 0:
+        raise Error(rc, what)
+
+
+# ---------------------------------------------------------------- presets / options
+
+class ChromaSubsamplingPreset(enum.IntEnum):
+    """src/image/subsampling.rs:11-55"""
+    P444 = 0
+    P422 = 1
+    P420 = 2
+
+    def horizontal_rate(self) -> int:
+        return 1 if self == ChromaSubsamplingPreset.P444 else 2
+
+    def vertical_rate(self) -> int:
+        return 2 if self == ChromaSubsamplingPreset.P420 else 1
+
+
+class QuantizationTablePreset(enum.IntEnum):
+    """src/image/writer/jpeg/quantization_tables.rs:232-284 (names and aliases)"""
+    Specification = 0
+    Flat = 1
+    MSSIMKodakTuned = 2
+    PSNRHVSNKodakTuned = 3
+    DCTunePerceptualOptimization = 4
+    AVisualDetectionModel = 5
+    AnImprovedDetectionModel = 6
+
+    @classmethod
+    def from_name(cls, s: str) -> "QuantizationTablePreset":
+        names = {
+            "Specification": 0, "Spec": 0, "Default": 0, "0": 0, "Flat": 1, "1": 1, "MSSIM-Kodak-Tuned": 2, "2": 2,
+            "PSNR-HVS-N-Kodak-Tuned": 3, "4": 3, "DCTune-Perceptual-Optimization": 4, "6": 4,
+            "A-visual-detection-model": 5, "7": 5, "An-improved-detection-model": 6, "8": 6,
+        }
+        if s not in names:
+            raise ValueError(f"invalid quantization table preset '{s}'")
+        return cls(names[s])
+
+    def to_pair(self):
+        """QuantizationTablePreset::to_pair (quantization_tables.rs:286-327): (luma, chroma) natural order."""
+        return quantization_preset(int(self))
+
+
+def quantization_preset(preset: int):
+    L = (ctypes.c_uint8 * 64)()
+    C = (ctypes.c_uint8 * 64)()
+    _check(lib().dmmt_quantization_preset(int(preset), L, C), "quantization preset")
+    return list(L), list(C)
+
+
+def quality_tables(quality: int):
+    """Extension: IJG quality scaling of the Annex K tables (q50 == Specification)."""
+    L = (ctypes.c_uint8 * 64)()
+    C = (ctypes.c_uint8 * 64)()
+    _check(lib().dmmt_quality_tables(int(quality), L, C), "quality tables")
+    return list(L), list(C)
+
+
+@dataclass
+class JpegTransformationOptions:
+    """src/image/writer/jpeg.rs:31-39; tables may be given explicitly (quality extension)."""
+    chroma_subsampling_preset: ChromaSubsamplingPreset = ChromaSubsamplingPreset.P420
+    bits_per_channel: int = 8
+    quantization_table_preset: QuantizationTablePreset = QuantizationTablePreset.Specification
+    luma_table: list | None = None
+    chroma_table: list | None = None
+    restart_interval: int = 0
+    number_of_threads: int = 1
+
+    def to_c(self) -> DmmtOptions:
+        o = DmmtOptions()
+        o.subsampling = int(self.chroma_subsampling_preset)
+        o.bits_per_channel = int(self.bits_per_channel)
+        if self.luma_table is not None:
+            lq, cq = self.luma_table, self.chroma_table
+        else:
+            lq, cq = QuantizationTablePreset(self.quantization_table_preset).to_pair()
+        for i in range(64):
+            o.luma_q[i] = int(lq[i])
+            o.chroma_q[i] = int(cq[i])
+        o.n_threads = int(self.number_of_threads)
+        o.restart_interval = int(self.restart_interval)
+        return o
+
+
+# ---------------------------------------------------------------- image
+
+@dataclass
+class Image:
+    """Image (src/image.rs:7-11) kept as raw samples + maxval; the GPU applies
+    ``v as f32 / max as f32`` (color.rs:45-53)."""
+    width: int
+    height: int
+    maxval: int
+    samples: np.ndarray  # (height, width, 3) uint8 or uint16
+
+    @classmethod
+    def from_array(cls, rgb, maxval: int = 255) -> "Image":
+        a = np.asarray(rgb)
+        if a.ndim != 3 or a.shape[2] != 3:
+            raise ValueError("rgb must be (height, width, 3)")
+        dt = np.uint8 if maxval <= 255 and (a.size == 0 or a.max() <= 255) else np.uint16
+        return cls(a.shape[1], a.shape[0], int(maxval), np.ascontiguousarray(a, dtype=dt))
+
+    def to_c(self) -> DmmtImage:
+        s = self.samples
+        im = DmmtImage()
+        im.width, im.height, im.maxval = self.width, self.height, self.maxval
+        im.sample_bytes = s.dtype.itemsize
+        im.rgb = s.ctypes.data
+        return im
+
+
+def _image_from_c(im: DmmtImage) -> Image:
+    n = im.width * im.height * 3
+    dt = np.uint8 if im.sample_bytes == 1 else np.uint16
+    buf = (ctypes.c_uint8 * (n * im.sample_bytes)).from_address(im.rgb) if n else b""
+    arr = np.frombuffer(bytes(buf), dtype=dt).reshape(im.height, im.width, 3).copy()
+    lib().dmmt_free(im.rgb)
+    return Image(im.width, im.height, im.maxval, arr)
+
+
+class PPMImageReader:
+    """src/image/reader/ppm.rs:9-25 (P3 as the reference; P6 as an extension)."""
+
+    def __init__(self, reader):
+        self.reader = reader
+
+    def read_image(self) -> Image:
+        data = self.reader.read() if hasattr(self.reader, "read") else bytes(self.reader)
+        buf = ctypes.create_string_buffer(data, len(data))
+        im = DmmtImage()
+        _check(lib().dmmt_parse_ppm(ctypes.cast(buf, ctypes.c_void_p), len(data), ctypes.byref(im)), "read_image")
+        return _image_from_c(im)
+
+
+# ---------------------------------------------------------------- encoder
+
+class Encoder:
+    """A GPU context (dmmt_ctx): one device, one stream, pooled workspace.
+    Plays the role of the ThreadPool the reference passes around (lib.rs:62)."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = ctypes.c_void_p()
+        _check(lib().dmmt_ctx_create(int(device), ctypes.byref(self._ctx)), f"dmmt_ctx_create({device})")
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def close(self):
+        if self._ctx:
+            lib().dmmt_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- whole path
+    def encode(self, image: Image, options: JpegTransformationOptions) -> bytes:
+        return self.encode_batch([image], options)[0]
+
+    def encode_batch(self, images, options: JpegTransformationOptions):
+        n = len(images)
+        arr = (DmmtImage * n)(*[im.to_c() for im in images])
+        outs = (ctypes.c_void_p * n)()
+        lens = (ctypes.c_size_t * n)()
+        opt = options.to_c()
+        _check(lib().dmmt_jpeg_encode_batch(self._ctx, arr, n, ctypes.byref(opt), outs, lens), "encode")
+        res = []
+        for i in range(n):
+            res.append(ctypes.string_at(outs[i], lens[i]))
+            lib().dmmt_free(outs[i])
+        return res
+
+    # -- stages
+    def forward_blocks(self, image: Image, options: JpegTransformationOptions) -> np.ndarray:
+        hr = ChromaSubsamplingPreset(options.chroma_subsampling_preset).horizontal_rate()
+        vr = ChromaSubsamplingPreset(options.chroma_subsampling_preset).vertical_rate()
+        wp = -(-image.width // (8 * hr)) * 8 * hr
+        hp = -(-image.height // (8 * vr)) * 8 * vr
+        cap = (wp * hp) // 64 * 3
+        out = np.zeros((cap, 64), np.int16)
+        nb = ctypes.c_size_t()
+        opt = options.to_c()
+        im = image.to_c()
+        _check(lib().dmmt_forward_blocks(self._ctx, ctypes.byref(im), ctypes.byref(opt), out.ctypes.data, cap,
+                                         ctypes.byref(nb)), "forward_blocks")
+        return out[:nb.value].copy()
+
+    def encode_coefficients(self, coef_zz: np.ndarray, width: int, height: int,
+                            options: JpegTransformationOptions) -> bytes:
+        c = np.ascontiguousarray(coef_zz, dtype=np.int16)
+        out = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        opt = options.to_c()
+        _check(lib().dmmt_encode_coefficients(self._ctx, c.ctypes.data, c.shape[0], width, height, ctypes.byref(opt),
+                                              ctypes.byref(out), ctypes.byref(n)), "encode_coefficients")
+        data = ctypes.string_at(out.value, n.value)
+        lib().dmmt_free(out)
+        return data
+
+    def dct_transform(self, blocks: np.ndarray) -> np.ndarray:
+        """Discrete8x8CosineTransformer::transform_on_threadpool (cosine_transform.rs:55-73) on the GPU."""
+        a = np.ascontiguousarray(blocks, dtype=np.float32).copy()
+        _check(lib().dmmt_dct_transform(self._ctx, a.ctypes.data, a.size), "dct_transform")
+        return a
+
+    # -- device resident
+    def encode_device(self, d_rgb: int, n_frames: int, width: int, height: int, options: JpegTransformationOptions,
+                      d_out: int, out_stride: int, d_out_len: int, frame_stride: int | None = None, maxval: int = 255,
+                      sample_bytes: int = 1, stream: int | None = None, opt_c: DmmtOptions | None = None):
+        f = DmmtDeviceFrames()
+        f.d_rgb = d_rgb
+        f.frame_stride = frame_stride if frame_stride is not None else width * height * 3 * sample_bytes
+        f.n_frames = n_frames
+        f.width, f.height, f.maxval, f.sample_bytes = width, height, maxval, sample_bytes
+        f.d_out, f.out_stride, f.d_out_len = d_out, out_stride, d_out_len
+        opt = opt_c if opt_c is not None else options.to_c()
+        _check(lib().dmmt_encode_device(self._ctx, ctypes.byref(f), ctypes.byref(opt), stream), "encode_device")
+
+    def synchronize(self):
+        _check(lib().dmmt_ctx_synchronize(self._ctx), "synchronize")
+
+    def malloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        _check(lib().dmmt_device_malloc(self._ctx, nbytes, ctypes.byref(p)), "malloc")
+        return p.value
+
+    def free(self, ptr: int):
+        _check(lib().dmmt_device_free(self._ctx, ptr), "free")
+
+    def h2d(self, dst: int, src: np.ndarray):
+        s = np.ascontiguousarray(src)
+        _check(lib().dmmt_memcpy_h2d(self._ctx, dst, s.ctypes.data, s.nbytes), "h2d")
+
+    def d2h(self, src: int, nbytes: int) -> bytes:
+        buf = ctypes.create_string_buffer(nbytes)
+        _check(lib().dmmt_memcpy_d2h(self._ctx, ctypes.cast(buf, ctypes.c_void_p), src, nbytes), "d2h")
+        return buf.raw
+
+    def fill_synthetic(self, d_rgb: int, width: int, height: int, n_frames: int, first_frame: int = 0,
+                       seed: int = 0x9E3779B9):
+        _check(lib().dmmt_fill_synthetic(self._ctx, d_rgb, width, height, n_frames, first_frame, seed), "synthetic")
+
+    def set_profiling(self, on: bool):
+        _check(lib().dmmt_ctx_set_profiling(self._ctx, 1 if on else 0))
+
+    def profile(self):
+        n = lib().dmmt_num_stages()
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int32 * n)()
+        _check(lib().dmmt_ctx_profile(self._ctx, ms, cnt, n))
+        return {lib().dmmt_stage_name(i).decode(): (ms[i], cnt[i]) for i in range(n)}
+
+
+def max_jpeg_bytes(width: int, height: int, subsampling: int) -> int:
+    return lib().dmmt_max_jpeg_bytes(width, height, int(subsampling))
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    lib().dmmt_device_count(ctypes.byref(n))
+    return n.value
+
+
+class AraiDiscrete8x8CosineTransformer:
+    """The reference's pluggable DCT operator (cosine_transform.rs:13-73, arai.rs:95-104), on the GPU."""
+
+    def __init__(self, encoder: Encoder):
+        self.encoder = encoder
+
+    def transform(self, block) -> np.ndarray:
+        return self.encoder.dct_transform(np.asarray(block, np.float32).reshape(64)).reshape(64)
+
+    def transform_on_threadpool(self, channel: np.ndarray, jobs_chunk_size: int = 700) -> np.ndarray:
+        return self.encoder.dct_transform(channel)
+
+
+class JpegImageWriter:
+    """src/image/writer/jpeg.rs:41-75: ``JpegImageWriter::new(writer, image, options, pool).write_image()``."""
+
+    def __init__(self, writer, image: Image, options: JpegTransformationOptions, encoder: Encoder):
+        self.writer = writer
+        self.image = image
+        self.options = options
+        self.encoder = encoder
+
+    def write_image(self) -> None:
+        data = self.encoder.encode(self.image, self.options)
+        try:
+            self.writer.write(data)
+            if hasattr(self.writer, "flush"):
+                self.writer.flush()
+        except OSError as e:
+            raise Error(-16, str(e)) from e
+
+
+@dataclass
+class Arguments:
+    """src/lib.rs:35-42 / cli.rs defaults"""
+    input_file: str
+    output_file: str
+    bits_per_channel: int = 8
+    chroma_subsampling_preset: ChromaSubsamplingPreset = ChromaSubsamplingPreset.P420
+    number_of_threads: int = 1
+    quantization_table_preset: QuantizationTablePreset = QuantizationTablePreset.Specification
+    device: int = 0
+
+
+def convert_ppm_to_jpeg(arguments: Arguments, encoder: Encoder | None = None) -> None:
+    """src/lib.rs:59-77"""
+    try:
+        fin = open(arguments.input_file, "rb")
+    except FileNotFoundError as e:
+        raise Error(-7, arguments.input_file) from e
+    with fin:
+        try:
+            fout = open(arguments.output_file, "wb")
+        except OSError as e:
+            raise Error(-8, arguments.output_file) from e
+        with fout:
+            enc = encoder or Encoder(arguments.device)
+            image = PPMImageReader(fin).read_image()
+            opts = JpegTransformationOptions(arguments.chroma_subsampling_preset, arguments.bits_per_channel,
+                                             arguments.quantization_table_preset,
+                                             number_of_threads=arguments.number_of_threads)
+            JpegImageWriter(fout, image, opts, enc).write_image()
+
+
+def encode_array(rgb, maxval: int = 255, subsampling: int = 2, luma=None, chroma=None, preset: int = 0,
+                 encoder: Encoder | None = None, bits_per_channel: int = 8) -> bytes:
+    """Convenience: one image (HxWx3 array) -> JPEG bytes."""
+    enc = encoder or Encoder()
+    opts = JpegTransformationOptions(ChromaSubsamplingPreset(subsampling), bits_per_channel,
+                                     QuantizationTablePreset(preset), luma, chroma)
+    return enc.encode(Image.from_array(rgb, maxval), opts)
+
+
+__all__ = [
+    "Error", "LibraryMissing", "build", "lib", "ChromaSubsamplingPreset", "QuantizationTablePreset",
+    "JpegTransformationOptions", "Image", "PPMImageReader", "Encoder", "JpegImageWriter", "Arguments",
+    "convert_ppm_to_jpeg", "quantization_preset", "quality_tables", "max_jpeg_bytes", "device_count",
+    "AraiDiscrete8x8CosineTransformer", "encode_array", "io",
+]

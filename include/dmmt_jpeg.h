@@ -1,0 +1,188 @@
+/*
+ * dmmt_jpeg.h -- C ABI of the MI355X (gfx950) baseline-JPEG encode path.
+ *
+ * Drop-in boundary for SilverlightningY/dmmt-jpeg-encoder's encoder seam.  Every
+ * entry point names the reference interface it replaces (paths relative to the
+ * reference repository).  Plain C types only: no HIP, no torch types.  The
+ * reference's Rust host would bind these through an `extern "C"` block; see
+ * INTEGRATION.md for that binding.
+ *
+ * Return convention: 0 = OK, negative = error (dmmt_strerror).  Where the
+ * reference panics (value above maxval, category > 15, empty image) these
+ * functions return an error code instead; they never abort.
+ *
+ * Output bytes are identical to the reference CPU encoder's for the same image
+ * and options (restart_interval == 0).
+ */
+#ifndef DMMT_JPEG_H
+#define DMMT_JPEG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMMT_ABI_VERSION 1
+
+/* ---- error codes: the reference's error::Error variants (error.rs:3-22), in order,
+ *      then codes for states where the reference panics or that only a GPU has. */
+enum dmmt_status {
+    DMMT_OK = 0,
+    DMMT_E_PPM_MISSING_TOKEN = -1,          /* PPMFileDoesNotContainRequiredToken */
+    DMMT_E_PPM_PARSE_TOKEN = -2,            /* ParsingOfTokenFailed */
+    DMMT_E_PPM_INCOMPLETE_PIXEL = -3,       /* IncompletePixelParsed */
+    DMMT_E_PPM_SIZE_MISMATCH = -4,          /* MismatchOfSizeBetweenHeaderAndValues */
+    DMMT_E_INPUT_NOT_FOUND = -5,            /* InputFileNotFound */
+    DMMT_E_NO_READ_PERMISSION = -6,         /* NoReadPermissionForInputFile */
+    DMMT_E_OPEN_INPUT = -7,                 /* UnableToOpenInputFileForReading */
+    DMMT_E_OPEN_OUTPUT = -8,                /* UnableToOpenOutputFileForWriting */
+    DMMT_E_WRITE_START_OF_FILE = -9,        /* FailedToWriteStartOfFile */
+    DMMT_E_WRITE_HUFFMAN_TABLES = -10,      /* FailedToWriteHuffmanTables */
+    DMMT_E_WRITE_END_OF_FILE = -11,         /* FailedToWriteEndOfFile */
+    DMMT_E_WRITE_JFIF = -12,                /* FailedToWriteJfifApplicationHeader */
+    DMMT_E_WRITE_QUANTIZATION_TABLE = -13,  /* FailedToWriteQuantizationTable */
+    DMMT_E_WRITE_START_OF_FRAME = -14,      /* FailedToWriteStartOfFrame */
+    DMMT_E_WRITE_START_OF_SCAN = -15,       /* FailedToWriteStartOfScan */
+    DMMT_E_WRITE_IMAGE_DATA = -16,          /* FailedToWriteImageData */
+    DMMT_E_HUFFMAN_SYMBOL_MISSING = -17,    /* HuffmanSymbolNotPresentInTranslator */
+    DMMT_E_WRITE_BLOCK = -18,               /* FailedToWriteBlock */
+    /* reference panics */
+    DMMT_E_VALUE_EXCEEDS_MAX = -100,        /* color.rs:63-65 */
+    DMMT_E_CATEGORY_RANGE = -101,           /* categorize.rs:25-30 */
+    DMMT_E_INVALID_ARGUMENT = -102,         /* empty image, padded size > u16, bad option */
+    /* device */
+    DMMT_E_HIP = -200,                      /* a HIP runtime call failed */
+    DMMT_E_OUT_OF_MEMORY = -201,
+    DMMT_E_NO_DEVICE = -202,                /* no gfx950 device visible: there is no CPU fallback */
+    DMMT_E_CAPACITY = -203                  /* caller-provided device output buffer too small */
+};
+
+/* ChromaSubsamplingPreset (subsampling.rs:11-55) */
+enum dmmt_subsampling { DMMT_P444 = 0, DMMT_P422 = 1, DMMT_P420 = 2 };
+
+/* QuantizationTablePreset (quantization_tables.rs:232-327), in the reference's order */
+enum dmmt_quant_preset {
+    DMMT_Q_SPECIFICATION = 0,
+    DMMT_Q_FLAT = 1,
+    DMMT_Q_MSSIM_KODAK_TUNED = 2,
+    DMMT_Q_PSNR_HVS_N_KODAK_TUNED = 3,
+    DMMT_Q_DCTUNE_PERCEPTUAL_OPTIMIZATION = 4,
+    DMMT_Q_A_VISUAL_DETECTION_MODEL = 5,
+    DMMT_Q_AN_IMPROVED_DETECTION_MODEL = 6
+};
+
+/* Image<f32> (image.rs:7-11) before normalisation: the raw PPM samples and maxval
+ * (ppm.rs:145-163); the library reproduces `v as f32 / max as f32` (color.rs:45-53)
+ * on the device.  rgb is interleaved R,G,B, row-major, sample_bytes 1 (uint8) or 2
+ * (uint16, host endian). */
+typedef struct dmmt_image {
+    uint16_t width;
+    uint16_t height;
+    uint16_t maxval;
+    uint16_t sample_bytes;
+    const void* rgb;
+} dmmt_image;
+
+/* JpegTransformationOptions (jpeg.rs:31-39) with the table pair resolved. */
+typedef struct dmmt_options {
+    int32_t subsampling;      /* dmmt_subsampling; cli.rs default P420 */
+    int32_t bits_per_channel; /* 8/16/32, written into SOF only (encoder.rs:235) */
+    uint8_t luma_q[64];       /* natural (row-major) order, 1..255 */
+    uint8_t chroma_q[64];
+    int32_t n_threads;        /* the reference's CPU thread count (cli.rs:104-109); unused on GPU */
+    int32_t restart_interval; /* 0 = reference behaviour; >0 = DRI/RSTn every N MCUs (extension) */
+} dmmt_options;
+
+/* A batch of equally sized frames already resident in device memory (HBM). */
+typedef struct dmmt_device_frames {
+    const void* d_rgb;          /* n_frames frames, frame f at d_rgb + f * frame_stride */
+    size_t frame_stride;        /* bytes between frames */
+    int32_t n_frames;
+    uint16_t width, height, maxval, sample_bytes;
+    uint8_t* d_out;             /* JPEG f written at d_out + f * out_stride */
+    size_t out_stride;          /* >= dmmt_max_jpeg_bytes(width, height, subsampling) */
+    uint32_t* d_out_len;        /* device array [n_frames] of JPEG sizes */
+} dmmt_device_frames;
+
+typedef struct dmmt_ctx dmmt_ctx;
+
+/* ---- context ---------------------------------------------------------------------- */
+/* Replaces the ThreadPool the reference threads through convert_ppm_to_jpeg
+ * (lib.rs:62) and JpegImageWriter::new (jpeg.rs:48-62): owns one GPU, its stream and
+ * pooled device workspace.  Fails with DMMT_E_NO_DEVICE when no gfx950 GPU is visible. */
+int dmmt_ctx_create(int device, dmmt_ctx** out);
+void dmmt_ctx_destroy(dmmt_ctx* ctx);
+int dmmt_device_count(int* count);
+int dmmt_ctx_synchronize(dmmt_ctx* ctx);
+
+/* ---- the encoder seam --------------------------------------------------------------- */
+/* JpegImageWriter::write_image (jpeg.rs:64-75) = Transformer::transform
+ * (transformer.rs:188-221) + Encoder::encode (encoder.rs:125-135), whole path on the
+ * GPU.  *out is allocated by the library, free it with dmmt_free. */
+int dmmt_jpeg_encode(dmmt_ctx* ctx, const dmmt_image* img, const dmmt_options* opt, uint8_t** out,
+                     size_t* out_len);
+/* Many independent images in as few launches as possible (images of equal size share
+ * launches).  outs[i]/lens[i] as dmmt_jpeg_encode. */
+int dmmt_jpeg_encode_batch(dmmt_ctx* ctx, const dmmt_image* imgs, int n, const dmmt_options* opt,
+                           uint8_t** outs, size_t* lens);
+/* Device-resident form: frames in HBM -> JPEG files in HBM, enqueued on `stream`
+ * (a hipStream_t, NULL = the context's stream), no host synchronisation. */
+int dmmt_encode_device(dmmt_ctx* ctx, const dmmt_device_frames* frames, const dmmt_options* opt, void* stream);
+size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t subsampling);
+
+/* ---- stage-level entry points (parity tests) ---------------------------------------- */
+/* Front half only (transformer.rs:188-199): quantised zigzag blocks, MCU emission order
+ * (block_fold_iterator.rs:53-148), 64 int16 per block, into coef (host). */
+int dmmt_forward_blocks(dmmt_ctx* ctx, const dmmt_image* img, const dmmt_options* opt, int16_t* coef,
+                        size_t cap_blocks, size_t* nblocks);
+/* Back half only (transformer.rs:199-220 + encoder.rs:125-282): emission-order zigzag
+ * blocks (host) -> JPEG file. */
+int dmmt_encode_coefficients(dmmt_ctx* ctx, const int16_t* coef, size_t nblocks, uint16_t width,
+                             uint16_t height, const dmmt_options* opt, uint8_t** out, size_t* out_len);
+/* Discrete8x8CosineTransformer::transform_on_threadpool (cosine_transform.rs:55-73) with
+ * the Arai transformer (arai.rs:95-104): in-place 2-D DCT of every 64-float block of a
+ * host array, computed on the GPU.  len is the number of floats (multiple of 64). */
+int dmmt_dct_transform(dmmt_ctx* ctx, float* blocks, size_t len);
+
+/* ---- host helpers --------------------------------------------------------------------- */
+/* QuantizationTablePreset::to_pair (quantization_tables.rs:286-327), natural order */
+int dmmt_quantization_preset(int32_t preset, uint8_t luma[64], uint8_t chroma[64]);
+/* Extension: IJG quality scaling of the Annex K tables (quality 1..100; 50 = Specification) */
+int dmmt_quality_tables(int32_t quality, uint8_t luma[64], uint8_t chroma[64]);
+void dmmt_default_options(dmmt_options* opt); /* cli.rs defaults: P420, 8 bit, Specification */
+/* PPMImageReader::read_image (ppm.rs:19-25; P3 as the reference, plus binary P6).
+ * Samples are returned raw (uint16) with their maxval; free img->rgb with dmmt_free. */
+int dmmt_read_ppm(const char* path, dmmt_image* img);
+int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img);
+/* convert_ppm_to_jpeg (lib.rs:59-77): read PPM, encode on the GPU, write the file. */
+int dmmt_convert_ppm_to_jpeg(dmmt_ctx* ctx, const char* input_path, const char* output_path,
+                             const dmmt_options* opt);
+void dmmt_free(void* p);
+const char* dmmt_strerror(int code);
+/* name of the error variant as in error.rs ("MismatchOfSizeBetweenHeaderAndValues", ...) */
+const char* dmmt_error_name(int code);
+
+/* ---- measurement ---------------------------------------------------------------------- */
+/* When enabled, every dmmt_encode_device call records HIP events around each kernel on
+ * the stream it launches on; dmmt_ctx_profile returns the summed milliseconds per stage
+ * (stage names via dmmt_stage_name) and the number of recorded launches. */
+int dmmt_ctx_set_profiling(dmmt_ctx* ctx, int enable);
+int dmmt_ctx_profile(dmmt_ctx* ctx, double* ms, int32_t* launches, int n_stages);
+int dmmt_num_stages(void);
+const char* dmmt_stage_name(int stage);
+/* device memory for callers without their own allocator (bench, tests) */
+int dmmt_device_malloc(dmmt_ctx* ctx, size_t bytes, void** ptr);
+int dmmt_device_free(dmmt_ctx* ctx, void* ptr);
+int dmmt_memcpy_h2d(dmmt_ctx* ctx, void* dst, const void* src, size_t bytes);
+int dmmt_memcpy_d2h(dmmt_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* synthetic frames (SURVEY.md 8(d) generator) written straight into device memory */
+int dmmt_fill_synthetic(dmmt_ctx* ctx, void* d_rgb, uint16_t width, uint16_t height, int32_t n_frames,
+                        int32_t first_frame, uint32_t seed);
+const char* dmmt_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

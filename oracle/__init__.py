@@ -72,7 +72,7 @@ def lib():
         L.ref_code_lengths.restype = i32
         L.ref_code_lengths.argtypes = [ctypes.POINTER(ctypes.c_uint64), i32, ctypes.POINTER(u8), ctypes.POINTER(i32)]
         L.ref_assign_codes.argtypes = [ctypes.POINTER(u8), ctypes.POINTER(i32), i32, ctypes.POINTER(u16), ctypes.POINTER(u8)]
-        L.ref_subsample_resort.argtypes = [ctypes.POINTER(f32), i32, i32, i32, i32, i32, ctypes.POINTER(f32)]
+        L.ref_subsample_resort.argtypes = [ctypes.POINTER(f32), i32, i32, i32, i32, i32, i32, ctypes.POINTER(f32)]
         L.ref_forward.restype = i32
         L.ref_forward.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
         L.ref_encode_coefficients.restype = i32
@@ -229,10 +229,10 @@ def category_pattern(v: int, cat: int) -> int:
     return lib().ref_category_pattern(int(v), int(cat))
 
 
-def subsample_resort(plane: np.ndarray, hr: int, vr: int, average: bool) -> np.ndarray:
+def subsample_resort(plane: np.ndarray, hr: int, vr: int, average: bool, square: int = 8) -> np.ndarray:
     p = np.ascontiguousarray(plane, dtype=np.float32)
     h, w = p.shape
     out = np.zeros((h // vr) * (w // hr), dtype=np.float32)
-    lib().ref_subsample_resort(p.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), w, h, hr, vr, int(average),
+    lib().ref_subsample_resort(p.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), w, h, hr, vr, int(average), int(square),
                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
     return out

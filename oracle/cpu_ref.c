@@ -43,7 +43,7 @@ void ref_rgb_to_ycbcr(float r, float g, float b, float out[3]) {
  * -0.0 (Rust >= 1.83) which is the identity, so the first sample starts the
  * chain.  ChannelSquareResorter (238-310) scatters into 8x8 block-contiguous
  * order: idx = (row/8)*(rowlen*8) + (col/8)*64 + (row%8)*8 + col%8. */
-void ref_subsample_resort(const float* plane, int w, int h, int hr, int vr, int average, float* out) {
+void ref_subsample_resort(const float* plane, int w, int h, int hr, int vr, int average, int square, float* out) {
     int sw = w / hr, sh = h / vr;
     for (int sy = 0; sy < sh; ++sy) {
         int row = sy * vr;
@@ -72,7 +72,9 @@ void ref_subsample_resort(const float* plane, int w, int h, int hr, int vr, int 
                 }
                 v = acc / (float)(hr * vr);
             }
-            size_t idx = (size_t)(sy / 8) * ((size_t)sw * 8) + (size_t)(sx / 8) * 64 + (size_t)(sy % 8) * 8 + (sx % 8);
+            size_t sq = (size_t)square;
+            size_t idx = (size_t)(sy / square) * ((size_t)sw * sq) + (size_t)(sx / square) * sq * sq +
+                         (size_t)(sy % square) * sq + (size_t)(sx % square);
             out[idx] = v;
         }
     }
@@ -603,9 +605,9 @@ static int ref_forward_impl(const uint16_t* rgb, int width, int height, int maxv
     }
     float* bcb = by + ny;
     float* bcr = bcb + nc;
-    ref_subsample_resort(py, wp, hp, 1, 1, 0, by);
-    ref_subsample_resort(pcb, wp, hp, hr, vr, opt->preset != REF_P444, bcb);
-    ref_subsample_resort(pcr, wp, hp, hr, vr, opt->preset != REF_P444, bcr);
+    ref_subsample_resort(py, wp, hp, 1, 1, 0, 8, by);
+    ref_subsample_resort(pcb, wp, hp, hr, vr, opt->preset != REF_P444, 8, bcb);
+    ref_subsample_resort(pcr, wp, hp, hr, vr, opt->preset != REF_P444, 8, bcr);
     free(planes);
 
     /* transformer.rs:126-148: Arai DCT over all blocks (thread pool, 700-block jobs) */

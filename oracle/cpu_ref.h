@@ -63,7 +63,7 @@ void ref_assign_codes(const uint8_t* symbols, const int* lengths, int n, uint16_
 /* Subsample + resort one padded plane into 8x8 block-contiguous order
  * (subsampling.rs:102-310 with the presets of 33-54).  out holds
  * (w/hr)*(h/vr) floats. */
-void ref_subsample_resort(const float* plane, int w, int h, int hr, int vr, int average, float* out);
+void ref_subsample_resort(const float* plane, int w, int h, int hr, int vr, int average, int square, float* out);
 
 /* ---- whole-path entry points ---- */
 /* Front half: padded image -> quantized blocks, zigzag order, MCU emission order. */
