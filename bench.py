@@ -1,0 +1,205 @@
+"""Benchmark of the gfx950 baseline-JPEG encode path (BASELINE.json metric).
+
+One step = one pass of the whole encode path (pixels in HBM -> complete JPEG
+file in HBM: colour, subsampling, Arai DCT, quantisation, symbols, Huffman
+tables, bit packing, byte stuffing, headers) over one batch of synthetic frames.
+At N=1 the workload is BASELINE config 2: one 3840x2160 frame, 4:4:4, IJG
+quality 90.  With N GPUs every rank encodes its own frames (independent
+images: weak scaling, no data-path collective); the driver launches one process
+per GPU via torch.distributed.run.
+
+Prints ONE JSON line on rank 0.  `roofline` is measured live: HIP events around
+the dominant kernel (k_front) on the stream it is launched on, over the timed
+region.  `cpu_baseline` times the CPU restatement of the reference encoder
+(oracle/, C, the reference's DCT thread-pool structure) on a bounded sample of
+the same workload on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dmmt-jpeg-encoder_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (imported before the library: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+import dmmt_jpeg  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+CONFIGS = {
+    # name: (width, height, subsampling, quality, frames per step)
+    "4k444q90": (3840, 2160, 0, 90, 1),
+    "1080p420q75x256": (1920, 1080, 2, 75, 256),
+    "8k420q75": (7680, 4320, 2, 75, 1),
+}
+
+
+def stage_index(name):
+    L = dmmt_jpeg.lib()
+    for i in range(L.dmmt_num_stages()):
+        if L.dmmt_stage_name(i).decode() == name:
+            return i
+    raise KeyError(name)
+
+
+def cpu_baseline(rgb, sub, luma, chroma, budget_s):
+    """Oracle (C restatement, DCT on a thread pool like transformer.rs:126-148) on this host."""
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    oracle.encode(rgb[:64, :64], 255, sub, luma, chroma)  # load/build
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.encode(rgb, 255, sub, luma, chroma, threads=threads)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    h, w = rgb.shape[:2]
+    return {"value": round(n * w * h / dt / 1e6, 3), "unit": "Mpixel/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x {w}x{h} frame(s) of the same synthetic workload, {dt:.1f} s, oracle/cpu_ref.c "
+                      f"(C restatement of the reference encoder; DCT on {threads} threads in 700-block jobs, "
+                      f"other stages serial)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="4k444q90", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--distinct-frames", type=int, default=4)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+    dev = torch.device("cuda", local_rank) if torch.cuda.is_available() else None
+
+    def barrier_sync(enc):
+        if world > 1:
+            dist.barrier()
+        if dev is not None:
+            torch.cuda.synchronize(dev)
+        enc.synchronize()
+
+    w, h, sub, quality, fps = CONFIGS[args.config]
+    luma, chroma = dmmt_jpeg.quality_tables(quality)
+    opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
+                                               chroma_table=chroma)
+    opt_c = opts.to_c()
+    enc = dmmt_jpeg.Encoder(local_rank)
+
+    nslots = max(1, args.distinct_frames)
+    frame_bytes = w * h * 3
+    out_stride = (dmmt_jpeg.max_jpeg_bytes(w, h, sub) + 255) // 256 * 256
+    d_in = [enc.malloc(frame_bytes * fps) for _ in range(nslots)]
+    d_out = enc.malloc(out_stride * fps)
+    d_len = enc.malloc(4 * fps)
+    for s in range(nslots):  # distinct synthetic frames per slot and per rank
+        enc.fill_synthetic(d_in[s], w, h, fps, first_frame=(rank * nslots + s) * fps)
+
+    def step(i):
+        enc.encode_device(d_in[i % nslots], fps, w, h, None, d_out, out_stride, d_len, frame_stride=frame_bytes,
+                          opt_c=opt_c)
+
+    for i in range(args.warmup):
+        step(i)
+    barrier_sync(enc)
+
+    front = stage_index("front")
+    enc.set_profiling(1 << front)  # events around the dominant kernel only
+    barrier_sync(enc)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    barrier_sync(enc)
+    elapsed = time.perf_counter() - t0
+    prof = enc.profile()
+    enc.set_profiling(0)
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    lens = np.frombuffer(enc.d2h(d_len, 4 * fps), np.uint32)
+    jpeg_bytes = float(lens.mean())
+
+    if rank == 0:
+        pixels = w * h * fps * args.steps * world
+        value = pixels / elapsed / 1e6
+        front_ms, front_n = prof["front"]
+        avg_front_s = front_ms / 1e3 / max(front_n, 1)
+        # algorithmic bytes of one k_front launch: RGB in (3 B/px) + quantised coefficients
+        # out (2 B per coefficient: 64 per block)
+        ncoef_per_px = 3.0 if sub == 0 else (2.0 if sub == 1 else 1.5)
+        algo_bytes = fps * (w * h * 3 + w * h * ncoef_per_px * 2)
+        achieved = algo_bytes / avg_front_s / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("front_hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if args.cpu_seconds > 0:
+            from oracle.synth import synthetic  # numpy twin of the device generator
+            rgb = synthetic(w, h, frame=0)
+            cpu = cpu_baseline(rgb, sub, luma, chroma, args.cpu_seconds)
+        line = {
+            "metric": "Mpixel/s encoded (4K PPM, q=90)" if args.config == "4k444q90" else f"Mpixel/s encoded ({args.config})",
+            "value": round(value, 2),
+            "unit": "Mpixel/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{w}x{h} synthetic RGB u8, {['4:4:4', '4:2:2', '4:2:0'][sub]}, IJG quality {quality}, "
+                            f"{fps} frame(s) per step per GPU, pixels in HBM -> JPEG files in HBM",
+                "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
+                "frames_per_step": fps, "mean_jpeg_bytes": jpeg_bytes, "parallelism": f"independent frames x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_front",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "avg_launch_us": round(avg_front_s * 1e6, 2),
+                "algorithmic_bytes_per_launch": algo_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    for p in d_in + [d_out, d_len]:
+        enc.free(p)
+    enc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -52,6 +52,7 @@ struct dmmt_ctx {
     bool q_valid = false;
     // profiling
     bool profile = false;
+    uint32_t profile_mask = 0;
     std::vector<EventPair> pending;
     std::vector<hipEvent_t> free_events;
     double stage_ms[ST_COUNT] = {0};
@@ -172,9 +173,21 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     w->packed = (uint32_t*)c->packed.p;
     w->seg_ff = (uint32_t*)c->seg_ff.p;
     w->status = (int*)c->status.p;
+    w->norm_lut = nullptr;  // bound by prepare() after upload_tables
+    w->qtab = nullptr;
+    w->qtab_u8 = nullptr;
+    return DMMT_OK;
+}
+
+// workspace + tables for one launch batch; every table pointer is valid on return
+int prepare(dmmt_ctx* c, const Geom& g, int nf, const dmmt_options* opt, int sb, hipStream_t st, Work* w) {
+    int rc;
+    if ((rc = ensure_work(c, g, nf, w))) return rc;
+    if ((rc = upload_tables(c, opt, g.maxval, sb, st))) return rc;
     w->norm_lut = (const float*)c->lut.p;
     w->qtab = (const float*)c->qtab.p;
     w->qtab_u8 = (const uint8_t*)c->qtab_u8.p;
+    if (!w->norm_lut || !w->qtab || !w->qtab_u8) return DMMT_E_HIP;
     return DMMT_OK;
 }
 
@@ -210,7 +223,7 @@ struct StageTimer {
     hipStream_t st;
     hipEvent_t a = nullptr, b = nullptr;
     StageTimer(dmmt_ctx* c_, int s, hipStream_t st_) : c(c_), stage(s), st(st_) {
-        if (c->profile) {
+        if (c->profile && ((c->profile_mask >> s) & 1u)) {
             a = take_event(c);
             b = take_event(c);
             if (a) (void)hipEventRecord(a, st);
@@ -242,9 +255,7 @@ int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, 
                    const dmmt_options* opt, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st) {
     Work w;
     int rc;
-    if ((rc = ensure_work(c, g, nf, &w))) return rc;
-    if ((rc = upload_tables(c, opt, g.maxval, sb, st))) return rc;
-    w.norm_lut = (const float*)c->lut.p;
+    if ((rc = prepare(c, g, nf, opt, sb, st, &w))) return rc;
     {
         StageTimer t(c, ST_FRONT, st);
         HIP_TRY(launch_front(d_rgb, frame_stride, sb, nf, g, w, st));
@@ -437,9 +448,7 @@ extern "C" int dmmt_forward_blocks(dmmt_ctx* c, const dmmt_image* img, const dmm
     const size_t frame_bytes = (size_t)img->width * img->height * 3 * img->sample_bytes;
     Work w;
     if ((rc = ensure(c->in, frame_bytes))) return rc;
-    if ((rc = ensure_work(c, g, 1, &w))) return rc;
-    if ((rc = upload_tables(c, opt, g.maxval, img->sample_bytes, st))) return rc;
-    w.norm_lut = (const float*)c->lut.p;
+    if ((rc = prepare(c, g, 1, opt, img->sample_bytes, st, &w))) return rc;
     HIP_TRY(hipMemcpyAsync(c->in.p, img->rgb, frame_bytes, hipMemcpyHostToDevice, st));
     {
         StageTimer t(c, ST_FRONT, st);
@@ -464,8 +473,7 @@ extern "C" int dmmt_encode_coefficients(dmmt_ctx* c, const int16_t* coef, size_t
     if ((rc = set_device(c))) return rc;
     hipStream_t st = c->stream;
     Work w;
-    if ((rc = ensure_work(c, g, 1, &w))) return rc;
-    if ((rc = upload_tables(c, opt, 255, 1, st))) return rc;
+    if ((rc = prepare(c, g, 1, opt, 1, st, &w))) return rc;
     const size_t out_stride = max_jpeg_bytes(g);
     if ((rc = ensure(c->out, out_stride))) return rc;
     if ((rc = ensure(c->out_len, 4))) return rc;
@@ -594,6 +602,7 @@ extern "C" int dmmt_ctx_set_profiling(dmmt_ctx* c, int enable) {
     std::lock_guard<std::mutex> lk(c->mu);
     drain_events(c);
     c->profile = enable != 0;
+    c->profile_mask = enable == 1 ? 0xFFFFFFFFu : (uint32_t)enable;  // 1 = every stage, else a stage bitmask
     for (int i = 0; i < ST_COUNT; ++i) {
         c->stage_ms[i] = 0;
         c->stage_launches[i] = 0;

@@ -165,9 +165,10 @@ const char* dmmt_strerror(int code);
 const char* dmmt_error_name(int code);
 
 /* ---- measurement ---------------------------------------------------------------------- */
-/* When enabled, every dmmt_encode_device call records HIP events around each kernel on
- * the stream it launches on; dmmt_ctx_profile returns the summed milliseconds per stage
- * (stage names via dmmt_stage_name) and the number of recorded launches. */
+/* enable = 0 off, 1 every stage, otherwise a bitmask of stages (bit s = stage s).  While
+ * on, every launch of a selected stage is bracketed by HIP events on the stream it is
+ * launched on; dmmt_ctx_profile returns the summed milliseconds per stage (stage names
+ * via dmmt_stage_name) and the number of recorded launches, and resets nothing. */
 int dmmt_ctx_set_profiling(dmmt_ctx* ctx, int enable);
 int dmmt_ctx_profile(dmmt_ctx* ctx, double* ms, int32_t* launches, int n_stages);
 int dmmt_num_stages(void);

@@ -55,17 +55,4 @@ def encoder():
     enc.close()
 
 
-def synthetic(w, h, frame=0, seed=0x9E3779B9, noise_bits=4):
-    """numpy twin of the device generator (kernels.hip k_synthetic)."""
-    y, x = np.mgrid[0:h, 0:w].astype(np.uint64)
-    base = (x + 8 * y) % 256
-    idx = (np.uint64(frame) * np.uint64(w * h) + y * np.uint64(w) + x) & np.uint64(0xFFFFFFFF)
-    s = (np.uint64(seed) ^ idx) & np.uint64(0xFFFFFFFF)
-    s = (s ^ (s << np.uint64(13))) & np.uint64(0xFFFFFFFF)
-    s = s ^ (s >> np.uint64(17))
-    s = (s ^ (s << np.uint64(5))) & np.uint64(0xFFFFFFFF)
-    m = np.uint64((1 << noise_bits) - 1)
-    r = base + (s & m)
-    g = ((base + np.uint64(85 * frame) + (y >> np.uint64(3))) % 256) + ((s >> np.uint64(4)) & m)
-    b = ((np.uint64(255) - base + (x >> np.uint64(4))) % 256) + ((s >> np.uint64(8)) & m)
-    return np.minimum(np.stack([r, g, b], -1), 255).astype(np.uint8)
+from oracle.synth import synthetic  # noqa: E402,F401  (numpy twin of the device generator)
