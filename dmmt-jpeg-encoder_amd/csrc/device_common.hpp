@@ -1,0 +1,114 @@
+// device_common.hpp -- wave-level helpers and JPEG integer primitives shared by
+// the gfx950 kernels (64-lane wavefronts).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmmt {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned long long t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int bit_length(uint32_t v) { return v ? 32 - __clz((int)v) : 0; }
+
+// categorize.rs:22-32 category of a value (|v| <= 32767 here)
+__device__ __forceinline__ int category_of(int v) { return bit_length((uint32_t)(v < 0 ? -v : v)); }
+
+// categorize.rs:34-46: the `cat` low bits of the extra-bits pattern
+__device__ __forceinline__ uint32_t extra_bits(int v, int cat) {
+    uint32_t p = v > 0 ? (uint32_t)v : (uint32_t)(v - 1);
+    return cat ? (p & ((1u << cat) - 1u)) : 0u;
+}
+
+// Relaxed agent-scope accesses for the look-back status words (gfx950: sc1 loads
+// and stores, bypassing the non-coherent per-CU L1).  Each status word carries
+// its flag and its value in ONE naturally aligned 8-byte word written by ONE
+// store, so a reader that sees the flag sees the value (MI355X_MICROARCH.md
+// "Valid forms", R2 granules).
+__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long lb_load(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// look-back status word: [63:62] flag (0 none, 1 aggregate, 2 inclusive prefix), [61:0] value
+constexpr unsigned long long kLbAgg = 1ull << 62;
+constexpr unsigned long long kLbPre = 2ull << 62;
+constexpr unsigned long long kLbVal = (1ull << 62) - 1;
+constexpr unsigned kLbSpinLimit = 1u << 22;  // bounded spin: a stuck predecessor sets status bit 4
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Decoupled look-back, executed by ONE whole wave: publish `agg` for tile `t`,
+// then read the status words of 64 predecessors per step (one sc1 load per
+// lane), and stop at the closest inclusive prefix; if any nearer predecessor
+// has published nothing yet, re-read the window.  Returns the exclusive prefix
+// of tile t (the same value in every lane).  Tiles are handed out by an atomic
+// ticket in the order they start, so every predecessor is already resident and
+// never waits on a successor; the spin is bounded anyway (status bit 4).
+__device__ __forceinline__ unsigned long long lookback(unsigned long long* st, unsigned t, unsigned long long agg,
+                                                       int* status) {
+    const int lane = lane_id();
+    if (t == 0) {
+        if (lane == 0) lb_store(&st[0], kLbPre | agg);
+        return 0ull;
+    }
+    if (lane == 0) lb_store(&st[t], kLbAgg | agg);
+    unsigned long long excl = 0;
+    long long j = (long long)t - 1;  // nearest predecessor of the current window
+    unsigned spins = 0;
+    for (;;) {
+        const long long idx = j - lane;
+        const unsigned long long v = idx >= 0 ? lb_load(&st[idx]) : kLbPre;  // before tile 0: prefix 0
+        const unsigned long long flag = v & ~kLbVal;
+        const unsigned long long pre = __ballot(flag == kLbPre);
+        const unsigned long long none = __ballot(flag == 0);
+        const int pl = pre ? __ffsll((long long)pre) - 1 : 64;  // nearest inclusive prefix in the window
+        const unsigned long long upto = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
+        if (none & upto) {
+            if (++spins > kLbSpinLimit) {
+                if (lane == 0) atomicOr(status, 4);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += wave_sum_u64(lane <= pl ? (v & kLbVal) : 0ull);
+        if (pl < 64) break;
+        j -= 64;
+    }
+    if (lane == 0) lb_store(&st[t], kLbPre | (excl + agg));
+    return excl;
+}
+
+}  // namespace dmmt

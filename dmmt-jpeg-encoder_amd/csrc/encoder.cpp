@@ -21,9 +21,7 @@ using namespace dmmt;
 
 namespace {
 
-const char* kStageNames[ST_COUNT] = {"front",       "dcdiff",     "tables",      "bits",
-                                     "scan",        "pack",       "stuff_count", "stuff_scan",
-                                     "stuff_write", "ac_hist"};
+const char* kStageNames[ST_COUNT] = {"front", "dcdiff", "tables", "pack", "stuff", "ac_hist"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -42,8 +40,8 @@ struct dmmt_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grown on demand, never shrunk)
-    DevBuf coef, dc, dcdiff, block_bits, chunk_bits, chunk_off, ac_hist, dc_hist, code_tab, hdr_len, total_bits,
-        packed, seg_ff, status, lut, qtab, qtab_u8;
+    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_bits, packed, tickets, lb_pack, lb_stuff,
+        status, lut, qtab, qtab_u8;
     // host-API staging
     DevBuf in, out, out_len, dct;
     // uploaded table state
@@ -148,30 +146,30 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     if ((rc = ensure(c->coef, nb * 64 * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dc, nb * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dcdiff, nb * sizeof(int16_t)))) return rc;
-    if ((rc = ensure(c->block_bits, nb * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c->chunk_bits, nch * 8))) return rc;
-    if ((rc = ensure(c->chunk_off, nch * 8))) return rc;
+    if ((rc = ensure(c->tickets, (size_t)nf * 2 * sizeof(unsigned)))) return rc;
+    if ((rc = ensure(c->lb_pack, nch * 8))) return rc;
+    if ((rc = ensure(c->lb_stuff, (size_t)nf * (size_t)g.nseg_cap * 8))) return rc;
     if ((rc = ensure(c->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
     if ((rc = ensure(c->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
     if ((rc = ensure(c->code_tab, (size_t)nf * 1024 * 4))) return rc;
     if ((rc = ensure(c->hdr_len, (size_t)nf * 4))) return rc;
     if ((rc = ensure(c->total_bits, (size_t)nf * 8))) return rc;
-    if ((rc = ensure(c->packed, (size_t)nf * (size_t)g.packed_words * 4))) return rc;
-    if ((rc = ensure(c->seg_ff, (size_t)nf * (size_t)g.nseg_cap * 4))) return rc;
+    // k_pack ORs the chunk-edge words into this buffer and k_stuff zeroes what it read:
+    // it is all zero between launches, starting with the allocation
+    if ((rc = ensure(c->packed, (size_t)nf * (size_t)g.packed_words * 4, true))) return rc;
     if ((rc = ensure(c->status, 16, true))) return rc;
     w->coef = (int16_t*)c->coef.p;
     w->dc = (int16_t*)c->dc.p;
     w->dcdiff = (int16_t*)c->dcdiff.p;
-    w->block_bits = (uint32_t*)c->block_bits.p;
-    w->chunk_bits = (unsigned long long*)c->chunk_bits.p;
-    w->chunk_off = (unsigned long long*)c->chunk_off.p;
+    w->tickets = (unsigned*)c->tickets.p;
+    w->lb_pack = (unsigned long long*)c->lb_pack.p;
+    w->lb_stuff = (unsigned long long*)c->lb_stuff.p;
     w->ac_hist = (uint32_t*)c->ac_hist.p;
     w->dc_hist = (uint32_t*)c->dc_hist.p;
     w->code_tab = (uint32_t*)c->code_tab.p;
     w->hdr_len = (uint32_t*)c->hdr_len.p;
     w->total_bits = (unsigned long long*)c->total_bits.p;
     w->packed = (uint32_t*)c->packed.p;
-    w->seg_ff = (uint32_t*)c->seg_ff.p;
     w->status = (int*)c->status.p;
     w->norm_lut = nullptr;  // bound by prepare() after upload_tables
     w->qtab = nullptr;
@@ -238,15 +236,25 @@ struct StageTimer {
     }
 };
 
-// Enqueue the entropy back half (k_dcdiff .. k_stuff_write) for coefficients
-// already in w.coef / w.dc with AC histograms accumulated.
+// Enqueue the entropy back half (k_dcdiff, k_tables, k_pack, k_stuff) for
+// coefficients already in w.coef / w.dc with AC histograms accumulated.
 int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bits, uint8_t* out, size_t out_stride,
                       uint32_t* out_len, hipStream_t st) {
-    const Stage order[] = {ST_DCDIFF, ST_TABLES, ST_BITS, ST_SCAN, ST_PACK, ST_STUFF_COUNT, ST_STUFF_SCAN,
-                           ST_STUFF_WRITE};
-    for (Stage s : order) {
-        StageTimer t(c, s, st);
-        HIP_TRY(launch_stage(s, nf, g, w, bits, out, out_stride, out_len, st));
+    {
+        StageTimer t(c, ST_DCDIFF, st);
+        HIP_TRY(launch_dcdiff(nf, g, w, st));
+    }
+    {
+        StageTimer t(c, ST_TABLES, st);
+        HIP_TRY(launch_tables(nf, g, w, bits, out, out_stride, st));
+    }
+    {
+        StageTimer t(c, ST_PACK, st);
+        HIP_TRY(launch_pack(nf, g, w, st));
+    }
+    {
+        StageTimer t(c, ST_STUFF, st);
+        HIP_TRY(launch_stuff(nf, g, w, out, out_stride, out_len, st));
     }
     return DMMT_OK;
 }
@@ -270,8 +278,14 @@ int take_status(dmmt_ctx* c, hipStream_t st) {
     HIP_TRY(hipMemcpyAsync(&s, c->status.p, sizeof s, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (s) HIP_TRY(hipMemsetAsync(c->status.p, 0, sizeof(int), st));
+    if (s & (4 | 8 | 16)) {  // an aborted pack/stuff may leave packed words behind: restore the all-zero invariant
+        if (c->packed.p) HIP_TRY(hipMemsetAsync(c->packed.p, 0, c->packed.bytes, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     if (s & 1) return DMMT_E_VALUE_EXCEEDS_MAX;
     if (s & 2) return DMMT_E_HUFFMAN_SYMBOL_MISSING;
+    if (s & 4) return DMMT_E_HIP;
+    if (s & (8 | 16)) return DMMT_E_CAPACITY;
     return DMMT_OK;
 }
 
@@ -314,10 +328,10 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     drain_events(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
-    DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff, &c->block_bits, &c->chunk_bits, &c->chunk_off,
-                      &c->ac_hist,    &c->dc_hist,    &c->code_tab, &c->hdr_len,  &c->total_bits, &c->packed,
-                      &c->seg_ff,     &c->status,     &c->lut,    &c->qtab,       &c->qtab_u8,    &c->in,
-                      &c->out,        &c->out_len,    &c->dct};
+    DevBuf* bufs[] = {&c->coef,    &c->dc,       &c->dcdiff,  &c->ac_hist,  &c->dc_hist, &c->code_tab,
+                      &c->hdr_len, &c->total_bits, &c->packed, &c->tickets, &c->lb_pack, &c->lb_stuff,
+                      &c->status,  &c->lut,      &c->qtab,    &c->qtab_u8,  &c->in,      &c->out,
+                      &c->out_len, &c->dct};
     for (DevBuf* b : bufs) release(*b);
     (void)hipStreamDestroy(c->stream);
     delete c;

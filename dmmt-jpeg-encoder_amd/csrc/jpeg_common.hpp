@@ -57,7 +57,7 @@ inline Geom make_geom(int width, int height, int subsampling, int maxval, int re
     g.bpf = (long long)g.nmcu * g.bpm;
     g.nch = (int)((g.bpf + kChunkBlocks - 1) / kChunkBlocks);
     long long max_bits = g.bpf * kMaxBlockBits + 8LL * g.nmcu; // + restart padding
-    g.packed_words = (max_bits + 31) / 32 + 2;
+    g.packed_words = ((max_bits + 31) / 32 + 2 + 63) / 64 * 64;  // 256-byte aligned frame regions
     long long max_bytes = g.packed_words * 4;
     g.nseg_cap = (int)((max_bytes + kStuffSeg - 1) / kStuffSeg);
     return g;

@@ -15,12 +15,9 @@
 //               codes, JFIF header bytes [symbol_counting.rs:85-94,
 //               length_limited.rs:37-134, huffman/encoder.rs:45-157,
 //               encoder.rs:125-262]
-//  k_bits       bits per block and per chunk of kChunkBlocks blocks
-//  k_scan       per frame: exclusive scan of chunk bit counts
-//  k_pack       MSB-first bit packing at exact bit offsets [encoder.rs:264-404,
-//               binary_stream.rs:38-96]
-//  k_stuff_*    0xFF -> 0xFF 0x00 stuffing, 1-padding, EOI
-//               [segment_marker_injector.rs:13-30, binary_stream.rs:89-96]
+//  k_pack, k_stuff (entropy.hip)  bit packing at look-back offsets, byte
+//               stuffing, EOI [encoder.rs:264-404, binary_stream.rs:38-96,
+//               segment_marker_injector.rs:13-30]
 //
 // Floating point: this file is compiled with -ffp-contract=off and without
 // fast-math, f32 '/' is the correctly rounded IEEE division (hipcc default),
@@ -29,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "device_common.hpp"
 #include "jpeg_common.hpp"
 #include "kernels.hpp"
 
@@ -43,47 +41,6 @@ __constant__ uint8_t c_inv_zigzag[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4, 
                                          3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
                                          10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
                                          21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
-
-// ------------------------------------------------------------------ helpers
-
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
-
-__device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        unsigned long long t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
-
-__device__ __forceinline__ int bit_length(uint32_t v) { return v ? 32 - __clz((int)v) : 0; }
-
-// categorize.rs:22-32 category of a value (|v| <= 32767 here)
-__device__ __forceinline__ int category_of(int v) { return bit_length((uint32_t)(v < 0 ? -v : v)); }
-
-// categorize.rs:34-46: the `cat` low bits of the extra-bits pattern
-__device__ __forceinline__ uint32_t extra_bits(int v, int cat) {
-    uint32_t p = v > 0 ? (uint32_t)v : (uint32_t)(v - 1);
-    return cat ? (p & ((1u << cat) - 1u)) : 0u;
-}
 
 // quantizer.rs:60: round(d / q) half away from zero, Rust's saturating `as i16`
 __device__ __forceinline__ int16_t quantize(float d, float q) {
@@ -338,13 +295,21 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
 // DC difference per component in emission order (categorize.rs:153-169), with
 // the predictor reset at restart-interval starts (extension), + DC histograms.
 __global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, int16_t* __restrict__ dcdiff, Geom g,
-                                                uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/) {
+                                                uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
+                                                unsigned* __restrict__ tickets, unsigned long long* __restrict__ lb_pack,
+                                                unsigned long long* __restrict__ lb_stuff) {
     __shared__ uint32_t sH[32];
     const int tid = threadIdx.x;
     const int frame = blockIdx.y;
     if (tid < 32) sH[tid] = 0;
     __syncthreads();
     const long long base = (long long)frame * g.bpf;
+    // reset the work tickets and look-back words k_pack / k_stuff use in this launch
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nch; i += (long long)gridDim.x * 256)
+        lb_pack[(size_t)frame * g.nch + i] = 0ull;
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nseg_cap; i += (long long)gridDim.x * 256)
+        lb_stuff[(size_t)frame * g.nseg_cap + i] = 0ull;
+    if (blockIdx.x == 0 && tid < 2) tickets[tid * gridDim.y + frame] = 0u;
     for (long long el = (long long)blockIdx.x * 256 + tid; el < g.bpf; el += (long long)gridDim.x * 256) {
         const int m = (int)(el / g.bpm);
         const int k = (int)(el - (long long)m * g.bpm);
@@ -391,6 +356,7 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
                                                  const uint8_t* __restrict__ qtab_u8,  // [2][64] natural
                                                  int bits_per_channel, int* __restrict__ status) {
     __shared__ unsigned long long sFreq[4][256];
+    __shared__ unsigned long long sKey[4][256];
     __shared__ unsigned long long sSortF[4][256];
     __shared__ uint8_t sSortS[4][256];
     __shared__ unsigned long long sLev[2][4][512];
@@ -409,18 +375,18 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
 
     // ---- 1
     unsigned long long f = 0;
-    if (tab & 1) {
-        for (int r = 0; r < kHistReps; ++r) {
-            uint32_t* p = &ac_hist[(((size_t)frame * kHistReps + r) * 2 + (tab >> 1)) * 256 + s];
-            f += *p;
-            *p = 0;
-        }
-    } else if (s < 16) {
-        for (int r = 0; r < kHistReps; ++r) {
-            uint32_t* p = &dc_hist[((size_t)frame * kHistReps + r) * 32 + (tab >> 1) * 16 + s];
-            f += *p;
-            *p = 0;
-        }
+    if ((tab & 1) || s < 16) {
+        // all replica loads first (independent, in flight together), then the zeroing stores
+        uint32_t* p0 = (tab & 1) ? &ac_hist[(((size_t)frame * kHistReps) * 2 + (tab >> 1)) * 256 + s]
+                                 : &dc_hist[((size_t)frame * kHistReps) * 32 + (tab >> 1) * 16 + s];
+        const size_t rstride = (tab & 1) ? 512 : 32;
+        uint32_t v[kHistReps];
+#pragma unroll
+        for (int r = 0; r < kHistReps; ++r) v[r] = __builtin_nontemporal_load(p0 + r * rstride);
+#pragma unroll
+        for (int r = 0; r < kHistReps; ++r) f += v[r];
+#pragma unroll
+        for (int r = 0; r < kHistReps; ++r) p0[r * rstride] = 0u;
     }
     sFreq[tab][s] = f;
     if (s < 16) sBits[tab][s] = 0;
@@ -429,14 +395,19 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
     __syncthreads();
 
     // ---- 2
+    // key = (frequency, symbol), absent symbols last: rank = keys below mine
     int rank = -1;
-    if (f > 0) {
-        rank = 0;
-        for (int t = 0; t < 256; ++t) {
-            const unsigned long long ft = sFreq[tab][t];
-            rank += (ft > 0 && (ft < f || (ft == f && t < s))) ? 1 : 0;
+    {
+        const unsigned long long mykey = f ? ((f << 8) | (unsigned)s) : ~0ull;
+        sKey[tab][s] = mykey;
+        __syncthreads();
+        if (f > 0) {
+            int r = 0;
+#pragma unroll 16
+            for (int t = 0; t < 256; ++t) r += sKey[tab][t] < mykey ? 1 : 0;
+            rank = r;
+            atomicAdd(&sN[tab], 1);
         }
-        atomicAdd(&sN[tab], 1);
     }
     __syncthreads();
     const int n = sN[tab];
@@ -599,324 +570,6 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
     }
 }
 
-// ============================================================== entropy tokens
-// Lane i of a wave holds zigzag coefficient i of one block.  Pieces emitted by
-// the lane, in stream order (encoder.rs:356-404):
-//   lane 0        DC code + DC extra bits
-//   lane i>=1, c!=0  (run>>4) x ZRL code, then code(run&15, cat) + extra bits
-//   lane 63, c==0  EOB (trailing zeros, categorize.rs:147-149)
-struct LaneTok {
-    uint32_t main_val;  // code << cat | extra (right aligned)
-    int main_len;
-    int nzrl;
-    uint32_t zrl_code;
-    int zrl_len;
-    int eob;  // lane 63 only: main is the EOB code
-};
-
-__device__ __forceinline__ LaneTok lane_tokens(int lane, int c, unsigned long long nz, int dcd,
-                                               const uint32_t* __restrict__ dctab, const uint32_t* __restrict__ actab) {
-    LaneTok t{0u, 0, 0, 0u, 0, 0};
-    if (lane == 0) {
-        const int cat = category_of(dcd);
-        const uint32_t e = dctab[cat];
-        const int L = (int)(e >> 16);
-        t.main_val = ((e & 0xFFFFu) << cat) | extra_bits(dcd, cat);
-        t.main_len = L + cat;
-    } else if (c != 0) {
-        const unsigned long long below = nz & ((1ull << lane) - 1ull);
-        const int p = below ? 63 - __clzll(below) : 0;
-        const int run = lane - p - 1;
-        const int cat = category_of(c);
-        const uint32_t e = actab[((run & 15) << 4) | cat];
-        t.main_val = ((e & 0xFFFFu) << cat) | extra_bits(c, cat);
-        t.main_len = (int)(e >> 16) + cat;
-        t.nzrl = run >> 4;
-        if (t.nzrl) {
-            const uint32_t z = actab[0xF0];
-            t.zrl_code = z & 0xFFFFu;
-            t.zrl_len = (int)(z >> 16);
-        }
-    } else if (lane == 63) {
-        const uint32_t e = actab[0];
-        t.main_val = e & 0xFFFFu;
-        t.main_len = (int)(e >> 16);
-        t.eob = 1;
-    }
-    return t;
-}
-
-__device__ __forceinline__ int lane_bits(const LaneTok& t) { return t.nzrl * t.zrl_len + t.main_len; }
-
-// ============================================================== k_bits
-__global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, const int16_t* __restrict__ dcdiff,
-                                              const uint32_t* __restrict__ code_tab, Geom g,
-                                              uint32_t* __restrict__ block_bits, unsigned long long* __restrict__ chunk_bits) {
-    __shared__ uint32_t sTab[4 * 256];
-    __shared__ unsigned long long sPart[4];
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.y, chunk = blockIdx.x;
-    for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
-    __syncthreads();
-    const long long el0 = (long long)chunk * kChunkBlocks;
-    const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
-    const long long base = (long long)frame * g.bpf + el0;
-    unsigned long long acc = 0;
-    for (int b = wave; b < nb; b += 4) {
-        const long long e = base + b;
-        const int c = coef[e * 64 + lane];
-        const unsigned long long nz = __ballot(c != 0) & ~1ull;
-        const int k = (int)((el0 + b) % g.bpm);
-        const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
-        const int dcd = lane == 0 ? (int)dcdiff[e] : 0;
-        const LaneTok t = lane_tokens(lane, c, nz, dcd, tb, tb + 256);
-        const uint32_t sum = wave_sum_u32((uint32_t)lane_bits(t));
-        if (lane == 0) block_bits[e] = sum;
-        acc += sum;
-    }
-    if (lane == 0) sPart[wave] = acc;
-    __syncthreads();
-    if (tid == 0) chunk_bits[(size_t)frame * g.nch + chunk] = sPart[0] + sPart[1] + sPart[2] + sPart[3];
-}
-
-// ============================================================== k_scan
-// Per frame: exclusive scan of chunk bit counts -> chunk bit offsets; zero the
-// first and last word of every chunk (the only words two chunks can share; the
-// pack kernel ORs into them atomically and stores every other word plainly).
-__global__ __launch_bounds__(1024) void k_scan(const unsigned long long* __restrict__ chunk_bits,
-                                               unsigned long long* __restrict__ chunk_off,
-                                               unsigned long long* __restrict__ total_bits, Geom g,
-                                               uint32_t* __restrict__ packed) {
-    __shared__ unsigned long long sWave[16];
-    __shared__ unsigned long long sCarry;
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.x;
-    const unsigned long long* cb = chunk_bits + (size_t)frame * g.nch;
-    unsigned long long* co = chunk_off + (size_t)frame * g.nch;
-    uint32_t* pk = packed + (size_t)frame * g.packed_words;
-    if (tid == 0) sCarry = 0;
-    __syncthreads();
-    for (int base = 0; base < g.nch; base += 1024) {
-        const int i = base + tid;
-        const unsigned long long v = i < g.nch ? cb[i] : 0ull;
-        const unsigned long long incl = wave_incl_scan_u64(v);
-        if (lane == 63) sWave[wave] = incl;
-        __syncthreads();
-        unsigned long long wpre = 0;
-        for (int w = 0; w < wave; ++w) wpre += sWave[w];
-        const unsigned long long excl = sCarry + wpre + incl - v;
-        if (i < g.nch) {
-            co[i] = excl;
-            if (v > 0 && ((excl + v - 1) >> 5) < (unsigned long long)g.packed_words) {
-                pk[excl >> 5] = 0u;
-                pk[(excl + v - 1) >> 5] = 0u;
-            }
-        }
-        __syncthreads();
-        if (tid == 1023) sCarry = excl + v;
-        __syncthreads();
-    }
-    if (tid == 0) total_bits[frame] = sCarry;
-}
-
-// ============================================================== k_pack
-// One workgroup per chunk of kChunkBlocks blocks: block offsets by an in-group
-// scan of block_bits, one wave per block places each lane's pieces with LDS
-// atomicOr into an MSB-first word image of the chunk's bit range, then the
-// words go out byte-swapped (memory order = stream order).
-__device__ __forceinline__ void put_piece(uint32_t* w, unsigned long long pos, uint32_t val, int len) {
-    if (len <= 0) return;
-    const int off = (int)(pos & 31);
-    const unsigned long long v = (unsigned long long)val << (64 - off - len);
-    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-    const size_t wi = (size_t)(pos >> 5);
-    if (hi) atomicOr(&w[wi], hi);
-    if (lo) atomicOr(&w[wi + 1], lo);
-}
-
-__global__ __launch_bounds__(256) void k_pack(const int16_t* __restrict__ coef, const int16_t* __restrict__ dcdiff,
-                                              const uint32_t* __restrict__ code_tab, Geom g,
-                                              const uint32_t* __restrict__ block_bits,
-                                              const unsigned long long* __restrict__ chunk_off,
-                                              const unsigned long long* __restrict__ chunk_bits,
-                                              uint32_t* __restrict__ packed) {
-    constexpr int MAXW = (31 + kChunkBlocks * kMaxBlockBits + 63) / 32 + 1;
-    __shared__ uint32_t sW[MAXW];
-    __shared__ uint32_t sTab[4 * 256];
-    __shared__ uint32_t sOff[kChunkBlocks];
-    __shared__ uint32_t sWave[4];
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.y, chunk = blockIdx.x;
-    const long long el0 = (long long)chunk * kChunkBlocks;
-    const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
-    const long long base = (long long)frame * g.bpf + el0;
-    const unsigned long long bit0 = chunk_off[(size_t)frame * g.nch + chunk];
-    const unsigned long long nbits = chunk_bits[(size_t)frame * g.nch + chunk];
-    const int shift = (int)(bit0 & 31);
-    // bounds guard: a chunk can never exceed kChunkBlocks * kMaxBlockBits bits
-    if (nbits > (unsigned long long)kChunkBlocks * kMaxBlockBits ||
-        ((bit0 + nbits + 31) >> 5) + 1 > (unsigned long long)g.packed_words)
-        return;
-    const int nw = (int)((shift + nbits + 31) >> 5);
-    for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
-    for (int i = tid; i < nw + 1; i += 256) sW[i] = 0u;
-    // block offsets within the chunk (kChunkBlocks <= 256: one value per thread)
-    {
-        const uint32_t v = tid < nb ? block_bits[base + tid] : 0u;
-        const uint32_t incl = wave_incl_scan_u32(v);
-        if (lane == 63) sWave[wave] = incl;
-        __syncthreads();
-        uint32_t pre = 0;
-        for (int w = 0; w < wave; ++w) pre += sWave[w];
-        if (tid < kChunkBlocks) sOff[tid] = pre + incl - v + (uint32_t)shift;
-    }
-    __syncthreads();
-    for (int b = wave; b < nb; b += 4) {
-        const long long e = base + b;
-        const int c = coef[e * 64 + lane];
-        const unsigned long long nz = __ballot(c != 0) & ~1ull;
-        const int k = (int)((el0 + b) % g.bpm);
-        const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
-        const int dcd = lane == 0 ? (int)dcdiff[e] : 0;
-        const LaneTok t = lane_tokens(lane, c, nz, dcd, tb, tb + 256);
-        const uint32_t nbl = (uint32_t)lane_bits(t);
-        const uint32_t incl = wave_incl_scan_u32(nbl);
-        unsigned long long pos = (unsigned long long)sOff[b] + (incl - nbl);
-        for (int z = 0; z < t.nzrl; ++z) {
-            put_piece(sW, pos, t.zrl_code, t.zrl_len);
-            pos += (unsigned long long)t.zrl_len;
-        }
-        put_piece(sW, pos, t.main_val, t.main_len);
-    }
-    __syncthreads();
-    uint32_t* pk = packed + (size_t)frame * g.packed_words + (bit0 >> 5);
-    for (int i = tid; i < nw; i += 256) {
-        const uint32_t v = __builtin_bswap32(sW[i]);
-        if (i == 0 || i == nw - 1)
-            atomicOr(&pk[i], v);
-        else
-            pk[i] = v;
-    }
-}
-
-// ============================================================== stuffing
-// Packed scan bytes -> output bytes after the header, 0x00 after every 0xFF,
-// last partial byte padded with 1-bits (binary_stream.rs:89-96), EOI.
-__device__ __forceinline__ uint8_t scan_byte(const uint8_t* pb, unsigned long long i, unsigned long long nbytes,
-                                             int pad_bits) {
-    uint8_t v = pb[i];
-    if (i == nbytes - 1 && pad_bits) v |= (uint8_t)((1u << pad_bits) - 1u);
-    return v;
-}
-
-__global__ __launch_bounds__(256) void k_stuff_count(const uint32_t* __restrict__ packed,
-                                                     const unsigned long long* __restrict__ total_bits, Geom g,
-                                                     uint32_t* __restrict__ seg_ff) {
-    __shared__ uint32_t sWave[4];
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.y;
-    const unsigned long long tb = total_bits[frame];
-    const unsigned long long nbytes = (tb + 7) >> 3;
-    const int pad = (int)((8 - (tb & 7)) & 7);
-    const int nseg = (int)((nbytes + kStuffSeg - 1) / kStuffSeg);
-    const uint8_t* pb = reinterpret_cast<const uint8_t*>(packed + (size_t)frame * g.packed_words);
-    if (nbytes > (unsigned long long)g.packed_words * 4) return;
-    for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-        uint32_t cnt = 0;
-        const unsigned long long b0 = (unsigned long long)seg * kStuffSeg + tid * 16;
-        for (int j = 0; j < 16; ++j) {
-            const unsigned long long i = b0 + j;
-            if (i < nbytes) cnt += scan_byte(pb, i, nbytes, pad) == 0xFF;
-        }
-        cnt = wave_sum_u32(cnt);
-        if (lane == 0) sWave[wave] = cnt;
-        __syncthreads();
-        if (tid == 0) seg_ff[(size_t)frame * g.nseg_cap + seg] = sWave[0] + sWave[1] + sWave[2] + sWave[3];
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_stuff_scan(uint32_t* __restrict__ seg_ff,  // in: counts, out: offsets
-                                                     const unsigned long long* __restrict__ total_bits,
-                                                     const uint32_t* __restrict__ hdr_len, Geom g,
-                                                     uint8_t* __restrict__ out, size_t out_stride,
-                                                     uint32_t* __restrict__ out_len) {
-    __shared__ uint32_t sWave[16];
-    __shared__ uint32_t sCarry;
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.x;
-    const unsigned long long tb = total_bits[frame];
-    const unsigned long long nbytes = (tb + 7) >> 3;
-    const int nseg = (int)((nbytes + kStuffSeg - 1) / kStuffSeg);
-    uint32_t* sf = seg_ff + (size_t)frame * g.nseg_cap;
-    if (tid == 0) sCarry = 0;
-    __syncthreads();
-    for (int base = 0; base < nseg; base += 1024) {
-        const int i = base + tid;
-        const uint32_t v = i < nseg ? sf[i] : 0u;
-        const uint32_t incl = wave_incl_scan_u32(v);
-        if (lane == 63) sWave[wave] = incl;
-        __syncthreads();
-        uint32_t wpre = 0;
-        for (int w = 0; w < wave; ++w) wpre += sWave[w];
-        const uint32_t excl = sCarry + wpre + incl - v;
-        if (i < nseg) sf[i] = excl;
-        __syncthreads();
-        if (tid == 1023) sCarry = excl + v;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        const unsigned long long total = (unsigned long long)hdr_len[frame] + nbytes + sCarry;
-        uint8_t* o = out + (size_t)frame * out_stride;
-        if (total + 2 <= out_stride && nbytes <= (unsigned long long)g.packed_words * 4) {
-            o[total] = 0xFF;  // EOI (encoder.rs:131)
-            o[total + 1] = 0xD9;
-            out_len[frame] = (uint32_t)(total + 2);
-        } else {
-            out_len[frame] = 0;  // reported as DMMT_E_CAPACITY by the host
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void k_stuff_write(const uint32_t* __restrict__ packed,
-                                                     const unsigned long long* __restrict__ total_bits,
-                                                     const uint32_t* __restrict__ seg_off,
-                                                     const uint32_t* __restrict__ hdr_len, Geom g,
-                                                     uint8_t* __restrict__ out, size_t out_stride) {
-    __shared__ uint32_t sWave[4];
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.y;
-    const unsigned long long tb = total_bits[frame];
-    const unsigned long long nbytes = (tb + 7) >> 3;
-    const int pad = (int)((8 - (tb & 7)) & 7);
-    const int nseg = (int)((nbytes + kStuffSeg - 1) / kStuffSeg);
-    const uint8_t* pb = reinterpret_cast<const uint8_t*>(packed + (size_t)frame * g.packed_words);
-    uint8_t* o = out + (size_t)frame * out_stride + hdr_len[frame];
-    if (nbytes > (unsigned long long)g.packed_words * 4 || hdr_len[frame] + 2 * nbytes + 2 > out_stride) return;
-    for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-        const unsigned long long b0 = (unsigned long long)seg * kStuffSeg + tid * 16;
-        uint8_t v[16];
-        uint32_t cnt = 0;
-        for (int j = 0; j < 16; ++j) {
-            const unsigned long long i = b0 + j;
-            v[j] = i < nbytes ? scan_byte(pb, i, nbytes, pad) : 0;
-            cnt += (i < nbytes && v[j] == 0xFF);
-        }
-        const uint32_t incl = wave_incl_scan_u32(cnt);
-        if (lane == 63) sWave[wave] = incl;
-        __syncthreads();
-        uint32_t pre = seg_off[(size_t)frame * g.nseg_cap + seg];
-        for (int w = 0; w < wave; ++w) pre += sWave[w];
-        unsigned long long dst = b0 + pre + (incl - cnt);
-        for (int j = 0; j < 16; ++j) {
-            if (b0 + j >= nbytes) break;
-            o[dst++] = v[j];
-            if (v[j] == 0xFF) o[dst++] = 0x00;
-        }
-        __syncthreads();
-    }
-}
-
 // ============================================================== operator: DCT only
 // Discrete8x8CosineTransformer::transform over a block-contiguous f32 array
 // (cosine_transform.rs:55-73, arai.rs:95-104); one lane per row, then column.
@@ -1069,49 +722,18 @@ hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_stage(Stage s, int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
-                        size_t out_stride, uint32_t* out_len, hipStream_t st) {
-    const int per_frame = 2048 / n_frames > 0 ? 2048 / n_frames : 1;
-    switch (s) {
-    case ST_DCDIFF: {
-        dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame / 2 > 0 ? per_frame / 2 : 1), n_frames);
-        hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist);
-        break;
-    }
-    case ST_TABLES:
-        hipLaunchKernelGGL(k_tables, dim3(n_frames), dim3(1024), 0, st, w.ac_hist, w.dc_hist, w.code_tab, out, out_stride,
-                           w.hdr_len, g, w.qtab_u8, bits_per_channel, w.status);
-        break;
-    case ST_BITS:
-        hipLaunchKernelGGL(k_bits, dim3(g.nch, n_frames), dim3(256), 0, st, (const int16_t*)w.coef,
-                           (const int16_t*)w.dcdiff, (const uint32_t*)w.code_tab, g, w.block_bits, w.chunk_bits);
-        break;
-    case ST_SCAN:
-        hipLaunchKernelGGL(k_scan, dim3(n_frames), dim3(1024), 0, st, (const unsigned long long*)w.chunk_bits,
-                           w.chunk_off, w.total_bits, g, w.packed);
-        break;
-    case ST_PACK:
-        hipLaunchKernelGGL(k_pack, dim3(g.nch, n_frames), dim3(256), 0, st, (const int16_t*)w.coef,
-                           (const int16_t*)w.dcdiff, (const uint32_t*)w.code_tab, g, (const uint32_t*)w.block_bits,
-                           (const unsigned long long*)w.chunk_off, (const unsigned long long*)w.chunk_bits, w.packed);
-        break;
-    case ST_STUFF_COUNT:
-        hipLaunchKernelGGL(k_stuff_count, dim3(clampi(g.nseg_cap, 1, per_frame), n_frames), dim3(256), 0, st,
-                           (const uint32_t*)w.packed, (const unsigned long long*)w.total_bits, g, w.seg_ff);
-        break;
-    case ST_STUFF_SCAN:
-        hipLaunchKernelGGL(k_stuff_scan, dim3(n_frames), dim3(1024), 0, st, w.seg_ff,
-                           (const unsigned long long*)w.total_bits, (const uint32_t*)w.hdr_len, g, out, out_stride,
-                           out_len);
-        break;
-    case ST_STUFF_WRITE:
-        hipLaunchKernelGGL(k_stuff_write, dim3(clampi(g.nseg_cap, 1, per_frame), n_frames), dim3(256), 0, st,
-                           (const uint32_t*)w.packed, (const unsigned long long*)w.total_bits,
-                           (const uint32_t*)w.seg_ff, (const uint32_t*)w.hdr_len, g, out, out_stride);
-        break;
-    default:
-        return hipErrorInvalidValue;
-    }
+hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
+    const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
+    dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
+    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist, w.tickets,
+                       w.lb_pack, w.lb_stuff);
+    return hipGetLastError();
+}
+
+hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
+                         size_t out_stride, hipStream_t st) {
+    hipLaunchKernelGGL(k_tables, dim3(n_frames), dim3(1024), 0, st, w.ac_hist, w.dc_hist, w.code_tab, out, out_stride,
+                       w.hdr_len, g, w.qtab_u8, bits_per_channel, w.status);
     return hipGetLastError();
 }
 

@@ -1,4 +1,4 @@
-// kernels.hpp -- host-side launchers of the gfx950 kernels (kernels.hip).
+// kernels.hpp -- host-side launchers of the gfx950 kernels (kernels.hip, entropy.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -7,47 +7,37 @@
 
 namespace dmmt {
 
-// Device workspace of one launch batch (see kernels.hip for each buffer's role).
+// Device workspace of one launch batch (see the kernels for each buffer's role).
 struct Work {
     int16_t* coef;                  // [frames][bpf][64] zigzag, emission order
     int16_t* dc;                    // [frames][bpf]
     int16_t* dcdiff;                // [frames][bpf]
-    uint32_t* block_bits;           // [frames][bpf]
-    unsigned long long* chunk_bits; // [frames][nch]
-    unsigned long long* chunk_off;  // [frames][nch]
     uint32_t* ac_hist;              // [frames][reps][2][256], zero between launches
     uint32_t* dc_hist;              // [frames][reps][2][16], zero between launches
     uint32_t* code_tab;             // [frames][4][256]  (len << 16) | code
     uint32_t* hdr_len;              // [frames]
     unsigned long long* total_bits; // [frames]
-    uint32_t* packed;               // [frames][packed_words]
-    uint32_t* seg_ff;               // [frames][nseg_cap]
-    int* status;
+    uint32_t* packed;               // [frames][packed_words], all zero between launches
+    unsigned* tickets;              // [2][frames] pack / stuff work tickets, zeroed by k_dcdiff
+    unsigned long long* lb_pack;    // [frames][nch] look-back words, zeroed by k_dcdiff
+    unsigned long long* lb_stuff;   // [frames][nseg_cap] look-back words, zeroed by k_dcdiff
+    int* status;                    // error bits: 1 value>max, 2 table, 4 look-back stuck, 8/16 capacity
     const float* norm_lut;          // maxval-normalisation table
     const float* qtab;              // [2][64] f32
     const uint8_t* qtab_u8;         // [2][64]
 };
 
-enum Stage {
-    ST_FRONT = 0,
-    ST_DCDIFF,
-    ST_TABLES,
-    ST_BITS,
-    ST_SCAN,
-    ST_PACK,
-    ST_STUFF_COUNT,
-    ST_STUFF_SCAN,
-    ST_STUFF_WRITE,
-    ST_AC_HIST,
-    ST_COUNT
-};
+enum Stage { ST_FRONT = 0, ST_DCDIFF, ST_TABLES, ST_PACK, ST_STUFF, ST_AC_HIST, ST_COUNT };
 
-// Launches one stage on `st`.  Return hipSuccess or the launch error.
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
                         const Work& w, hipStream_t st);
 hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_t st);
-hipError_t launch_stage(Stage s, int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
-                        size_t out_stride, uint32_t* out_len, hipStream_t st);
+hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
+                         size_t out_stride, hipStream_t st);
+hipError_t launch_pack(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+hipError_t launch_stuff(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride, uint32_t* out_len,
+                        hipStream_t st);
 hipError_t launch_dct_blocks(float* data, long long nblocks, hipStream_t st);
 hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_frame, uint32_t seed, hipStream_t st);
 
