@@ -70,12 +70,18 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 }
 
 // Decoupled look-back, executed by ONE whole wave: publish `agg` for tile `t`,
-// then read the status words of 64 predecessors per step (one sc1 load per
-// lane), and stop at the closest inclusive prefix; if any nearer predecessor
-// has published nothing yet, re-read the window.  Returns the exclusive prefix
-// of tile t (the same value in every lane).  Tiles are handed out by an atomic
-// ticket in the order they start, so every predecessor is already resident and
-// never waits on a successor; the spin is bounded anyway (status bit 4).
+// then read a window of 64 x kLbPerLane predecessor status words per step (all
+// sc1 loads in flight together; lane l holds window positions l*K .. l*K+K-1,
+// position 0 = tile t-1) and stop at the nearest inclusive prefix; if any nearer
+// predecessor has published nothing yet, re-read the window.  Wide windows
+// matter: when many tiles publish their aggregates at the same moment the walk
+// to the nearest prefix is one dependent round trip per window.  Returns the
+// exclusive prefix of tile t (the same value in every lane).  Tiles are handed
+// out by an atomic ticket in the order they start, so every predecessor is
+// already resident and never waits on a successor; the spin is bounded anyway
+// (status bit 4).
+constexpr int kLbPerLane = 16;
+
 __device__ __forceinline__ unsigned long long lookback(unsigned long long* st, unsigned t, unsigned long long agg,
                                                        int* status) {
     const int lane = lane_id();
@@ -88,14 +94,28 @@ __device__ __forceinline__ unsigned long long lookback(unsigned long long* st, u
     long long j = (long long)t - 1;  // nearest predecessor of the current window
     unsigned spins = 0;
     for (;;) {
-        const long long idx = j - lane;
-        const unsigned long long v = idx >= 0 ? lb_load(&st[idx]) : kLbPre;  // before tile 0: prefix 0
-        const unsigned long long flag = v & ~kLbVal;
-        const unsigned long long pre = __ballot(flag == kLbPre);
-        const unsigned long long none = __ballot(flag == 0);
-        const int pl = pre ? __ffsll((long long)pre) - 1 : 64;  // nearest inclusive prefix in the window
-        const unsigned long long upto = pl >= 63 ? ~0ull : ((2ull << pl) - 1ull);
-        if (none & upto) {
+        unsigned long long v[kLbPerLane];
+#pragma unroll
+        for (int k = 0; k < kLbPerLane; ++k) {
+            const long long idx = j - (long long)lane * kLbPerLane - k;
+            v[k] = idx >= 0 ? lb_load(&st[idx]) : kLbPre;  // before tile 0: prefix 0
+        }
+        int first_pre = kLbPerLane;  // first inclusive prefix within this lane's run
+        bool none_before = false;    // a "nothing published" word before it
+        unsigned long long part = 0; // values up to and including first_pre
+#pragma unroll
+        for (int k = 0; k < kLbPerLane; ++k) {
+            const unsigned long long flag = v[k] & ~kLbVal;
+            if (first_pre == kLbPerLane) {
+                none_before |= flag == 0;
+                part += v[k] & kLbVal;
+                if (flag == kLbPre) first_pre = k;
+            }
+        }
+        const unsigned long long pre = __ballot(first_pre < kLbPerLane);
+        const int pl = pre ? __ffsll((long long)pre) - 1 : 64;  // lane holding the nearest prefix
+        const bool stall = __any((lane <= pl) && none_before);
+        if (stall) {
             if (++spins > kLbSpinLimit) {
                 if (lane == 0) atomicOr(status, 4);
                 break;
@@ -103,9 +123,9 @@ __device__ __forceinline__ unsigned long long lookback(unsigned long long* st, u
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        excl += wave_sum_u64(lane <= pl ? (v & kLbVal) : 0ull);
+        excl += wave_sum_u64(lane <= pl ? part : 0ull);
         if (pl < 64) break;
-        j -= 64;
+        j -= 64 * kLbPerLane;
     }
     if (lane == 0) lb_store(&st[t], kLbPre | (excl + agg));
     return excl;

@@ -21,7 +21,7 @@ using namespace dmmt;
 
 namespace {
 
-const char* kStageNames[ST_COUNT] = {"front", "dcdiff", "tables", "pack", "stuff", "ac_hist"};
+const char* kStageNames[ST_COUNT] = {"front", "dcdiff", "tables", "bits", "place", "ffcount", "stuffwrite", "ac_hist"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -40,8 +40,8 @@ struct dmmt_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grown on demand, never shrunk)
-    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_bits, packed, tickets, lb_pack, lb_stuff,
-        status, lut, qtab, qtab_u8;
+    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_bits, packed, block_bits, chunk_bits,
+        super_bits, seg_ff, super_ff, status, lut, qtab, qtab_u8;
     // host-API staging
     DevBuf in, out, out_len, dct;
     // uploaded table state
@@ -146,9 +146,11 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     if ((rc = ensure(c->coef, nb * 64 * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dc, nb * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dcdiff, nb * sizeof(int16_t)))) return rc;
-    if ((rc = ensure(c->tickets, (size_t)nf * 2 * sizeof(unsigned)))) return rc;
-    if ((rc = ensure(c->lb_pack, nch * 8))) return rc;
-    if ((rc = ensure(c->lb_stuff, (size_t)nf * (size_t)g.nseg_cap * 8))) return rc;
+    if ((rc = ensure(c->block_bits, nb * sizeof(uint16_t)))) return rc;
+    if ((rc = ensure(c->chunk_bits, nch * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c->super_bits, (size_t)nf * (size_t)g.nsuper * 8))) return rc;
+    if ((rc = ensure(c->seg_ff, (size_t)nf * (size_t)g.nseg_cap * 4))) return rc;
+    if ((rc = ensure(c->super_ff, (size_t)nf * (size_t)g.nsuper_seg * 8))) return rc;
     if ((rc = ensure(c->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
     if ((rc = ensure(c->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
     if ((rc = ensure(c->code_tab, (size_t)nf * 1024 * 4))) return rc;
@@ -161,9 +163,11 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     w->coef = (int16_t*)c->coef.p;
     w->dc = (int16_t*)c->dc.p;
     w->dcdiff = (int16_t*)c->dcdiff.p;
-    w->tickets = (unsigned*)c->tickets.p;
-    w->lb_pack = (unsigned long long*)c->lb_pack.p;
-    w->lb_stuff = (unsigned long long*)c->lb_stuff.p;
+    w->block_bits = (uint16_t*)c->block_bits.p;
+    w->chunk_bits = (uint32_t*)c->chunk_bits.p;
+    w->super_bits = (unsigned long long*)c->super_bits.p;
+    w->seg_ff = (uint32_t*)c->seg_ff.p;
+    w->super_ff = (unsigned long long*)c->super_ff.p;
     w->ac_hist = (uint32_t*)c->ac_hist.p;
     w->dc_hist = (uint32_t*)c->dc_hist.p;
     w->code_tab = (uint32_t*)c->code_tab.p;
@@ -249,12 +253,20 @@ int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bit
         HIP_TRY(launch_tables(nf, g, w, bits, out, out_stride, st));
     }
     {
-        StageTimer t(c, ST_PACK, st);
-        HIP_TRY(launch_pack(nf, g, w, st));
+        StageTimer t(c, ST_BITS, st);
+        HIP_TRY(launch_bits(nf, g, w, st));
     }
     {
-        StageTimer t(c, ST_STUFF, st);
-        HIP_TRY(launch_stuff(nf, g, w, out, out_stride, out_len, st));
+        StageTimer t(c, ST_PLACE, st);
+        HIP_TRY(launch_place(nf, g, w, st));
+    }
+    {
+        StageTimer t(c, ST_FFCOUNT, st);
+        HIP_TRY(launch_ffcount(nf, g, w, st));
+    }
+    {
+        StageTimer t(c, ST_STUFFWRITE, st);
+        HIP_TRY(launch_stuffwrite(nf, g, w, out, out_stride, out_len, st));
     }
     return DMMT_OK;
 }
@@ -328,10 +340,11 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     drain_events(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
-    DevBuf* bufs[] = {&c->coef,    &c->dc,       &c->dcdiff,  &c->ac_hist,  &c->dc_hist, &c->code_tab,
-                      &c->hdr_len, &c->total_bits, &c->packed, &c->tickets, &c->lb_pack, &c->lb_stuff,
-                      &c->status,  &c->lut,      &c->qtab,    &c->qtab_u8,  &c->in,      &c->out,
-                      &c->out_len, &c->dct};
+    DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff,     &c->ac_hist,    &c->dc_hist,
+                      &c->code_tab,   &c->hdr_len,    &c->total_bits, &c->packed,     &c->block_bits,
+                      &c->chunk_bits, &c->super_bits, &c->seg_ff,     &c->super_ff,   &c->status,
+                      &c->lut,        &c->qtab,       &c->qtab_u8,    &c->in,         &c->out,
+                      &c->out_len,    &c->dct};
     for (DevBuf* b : bufs) release(*b);
     (void)hipStreamDestroy(c->stream);
     delete c;

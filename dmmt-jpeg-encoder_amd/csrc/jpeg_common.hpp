@@ -14,11 +14,13 @@ static constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 
 // Histogram replicas per frame: the front/DC kernels add their per-workgroup
 // histograms into replica (blockIdx.x % kHistReps) to spread atomic traffic.
 static constexpr int kHistReps = 16;
-// Blocks per entropy chunk (bit-count / pack kernels): one workgroup each.
-static constexpr int kChunkBlocks = 128;
+// Blocks per entropy chunk (k_bits / k_place): one workgroup each.
+static constexpr int kChunkBlocks = 64;
 // Worst-case entropy-coded bits of one block: DC code 16 + 12 extra bits, 63 AC
 // tokens of code 16 + 12 extra bits (|coef| <= 2048 for 8-bit-range input).
 static constexpr int kMaxBlockBits = 28 * 64;
+// Chunks (or stuffing segments) per "super" counter of the two-level offsets.
+static constexpr int kSuper = 64;
 // Bytes per segment of the byte-stuffing pass.
 static constexpr int kStuffSeg = 4096;
 // Upper bound of the header the table kernel writes (SOI..SOS incl. DRI).
@@ -35,7 +37,9 @@ struct Geom {
     int restart_interval;   // 0 = reference behaviour
     long long bpf;          // blocks per frame
     int nch;                // entropy chunks per frame
+    int nsuper;             // super counters over the chunks
     int nseg_cap;           // stuffing segments per frame (capacity)
+    int nsuper_seg;         // super counters over the segments
     long long packed_words; // words of the packed-bit buffer per frame
 };
 
@@ -56,10 +60,12 @@ inline Geom make_geom(int width, int height, int subsampling, int maxval, int re
     g.restart_interval = restart_interval;
     g.bpf = (long long)g.nmcu * g.bpm;
     g.nch = (int)((g.bpf + kChunkBlocks - 1) / kChunkBlocks);
+    g.nsuper = (g.nch + kSuper - 1) / kSuper;
     long long max_bits = g.bpf * kMaxBlockBits + 8LL * g.nmcu; // + restart padding
     g.packed_words = ((max_bits + 31) / 32 + 2 + 63) / 64 * 64;  // 256-byte aligned frame regions
     long long max_bytes = g.packed_words * 4;
     g.nseg_cap = (int)((max_bytes + kStuffSeg - 1) / kStuffSeg);
+    g.nsuper_seg = (g.nseg_cap + kSuper - 1) / kSuper;
     return g;
 }
 

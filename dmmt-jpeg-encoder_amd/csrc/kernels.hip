@@ -15,9 +15,9 @@
 //               codes, JFIF header bytes [symbol_counting.rs:85-94,
 //               length_limited.rs:37-134, huffman/encoder.rs:45-157,
 //               encoder.rs:125-262]
-//  k_pack, k_stuff (entropy.hip)  bit packing at look-back offsets, byte
-//               stuffing, EOI [encoder.rs:264-404, binary_stream.rs:38-96,
-//               segment_marker_injector.rs:13-30]
+//  k_bits, k_place, k_ffcount, k_stuffwrite (entropy.hip): bit packing at
+//               exact offsets, byte stuffing, EOI [encoder.rs:264-404,
+//               binary_stream.rs:38-96, segment_marker_injector.rs:13-30]
 //
 // Floating point: this file is compiled with -ffp-contract=off and without
 // fast-math, f32 '/' is the correctly rounded IEEE division (hipcc default),
@@ -296,20 +296,19 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
 // the predictor reset at restart-interval starts (extension), + DC histograms.
 __global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, int16_t* __restrict__ dcdiff, Geom g,
                                                 uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
-                                                unsigned* __restrict__ tickets, unsigned long long* __restrict__ lb_pack,
-                                                unsigned long long* __restrict__ lb_stuff) {
+                                                unsigned long long* __restrict__ super_bits,
+                                                unsigned long long* __restrict__ super_ff) {
     __shared__ uint32_t sH[32];
     const int tid = threadIdx.x;
     const int frame = blockIdx.y;
     if (tid < 32) sH[tid] = 0;
     __syncthreads();
     const long long base = (long long)frame * g.bpf;
-    // reset the work tickets and look-back words k_pack / k_stuff use in this launch
-    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nch; i += (long long)gridDim.x * 256)
-        lb_pack[(size_t)frame * g.nch + i] = 0ull;
-    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nseg_cap; i += (long long)gridDim.x * 256)
-        lb_stuff[(size_t)frame * g.nseg_cap + i] = 0ull;
-    if (blockIdx.x == 0 && tid < 2) tickets[tid * gridDim.y + frame] = 0u;
+    // reset the super counters k_bits / k_ffcount add into in this launch
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nsuper; i += (long long)gridDim.x * 256)
+        super_bits[(size_t)frame * g.nsuper + i] = 0ull;
+    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nsuper_seg; i += (long long)gridDim.x * 256)
+        super_ff[(size_t)frame * g.nsuper_seg + i] = 0ull;
     for (long long el = (long long)blockIdx.x * 256 + tid; el < g.bpf; el += (long long)gridDim.x * 256) {
         const int m = (int)(el / g.bpm);
         const int k = (int)(el - (long long)m * g.bpm);
@@ -725,8 +724,8 @@ hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_
 hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
     const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
-    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist, w.tickets,
-                       w.lb_pack, w.lb_stuff);
+    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist, w.super_bits,
+                       w.super_ff);
     return hipGetLastError();
 }
 

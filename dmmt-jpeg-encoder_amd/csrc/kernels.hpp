@@ -18,16 +18,18 @@ struct Work {
     uint32_t* hdr_len;              // [frames]
     unsigned long long* total_bits; // [frames]
     uint32_t* packed;               // [frames][packed_words], all zero between launches
-    unsigned* tickets;              // [2][frames] pack / stuff work tickets, zeroed by k_dcdiff
-    unsigned long long* lb_pack;    // [frames][nch] look-back words, zeroed by k_dcdiff
-    unsigned long long* lb_stuff;   // [frames][nseg_cap] look-back words, zeroed by k_dcdiff
-    int* status;                    // error bits: 1 value>max, 2 table, 4 look-back stuck, 8/16 capacity
+    uint16_t* block_bits;           // [frames][bpf] entropy-coded bits per block
+    uint32_t* chunk_bits;           // [frames][nch]
+    unsigned long long* super_bits; // [frames][nsuper], zeroed by k_dcdiff
+    uint32_t* seg_ff;               // [frames][nseg_cap] 0xFF bytes per stuffing segment
+    unsigned long long* super_ff;   // [frames][nsuper_seg], zeroed by k_dcdiff
+    int* status;                    // error bits: 1 value>max, 2 table, 8/16 capacity
     const float* norm_lut;          // maxval-normalisation table
     const float* qtab;              // [2][64] f32
     const uint8_t* qtab_u8;         // [2][64]
 };
 
-enum Stage { ST_FRONT = 0, ST_DCDIFF, ST_TABLES, ST_PACK, ST_STUFF, ST_AC_HIST, ST_COUNT };
+enum Stage { ST_FRONT = 0, ST_DCDIFF, ST_TABLES, ST_BITS, ST_PLACE, ST_FFCOUNT, ST_STUFFWRITE, ST_AC_HIST, ST_COUNT };
 
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
                         const Work& w, hipStream_t st);
@@ -35,9 +37,11 @@ hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_
 hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st);
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st);
-hipError_t launch_pack(int n_frames, const Geom& g, const Work& w, hipStream_t st);
-hipError_t launch_stuff(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride, uint32_t* out_len,
-                        hipStream_t st);
+hipError_t launch_bits(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+hipError_t launch_place(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+hipError_t launch_ffcount(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
+                             uint32_t* out_len, hipStream_t st);
 hipError_t launch_dct_blocks(float* data, long long nblocks, hipStream_t st);
 hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_frame, uint32_t seed, hipStream_t st);
 
