@@ -18,10 +18,10 @@
 //                EOI (encoder.rs:131), file size; zeroes the packed words it read so
 //                the next launch's k_place can OR into a clean buffer.
 //
-// Lane layout of the bit passes: 16 lanes per block, 4 blocks per wave; lane l
-// of a block owns zigzag positions 4l..4l+3 (one 8-byte load).  The previous
-// non-zero coefficient before a lane's first position comes from a ballot of
-// "lane has a non-zero" and one shuffle.
+// The bit passes run one thread per block (256 blocks per workgroup): the walk
+// over a block's 64 coefficients is serial by nature and cheapest as a fully
+// unrolled register loop; the workgroup scan of the block bit counts gives
+// every thread its exact bit position.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,68 +30,6 @@
 #include "kernels.hpp"
 
 namespace dmmt {
-
-static_assert(kChunkBlocks == 64, "one wave scans the block offsets of a chunk");
-
-// Token walk of one lane's 4 zigzag positions in stream order (encoder.rs:356-404),
-// without data-dependent branches so the 16 lanes of a block run in lockstep.
-// Position 0 = DC: code(cat(diff)) + extra bits.  A non-zero AC coefficient:
-// (run >> 4) ZRL codes, then code((run & 15) << 4 | cat) + extra bits
-// (categorize.rs:132-151).  Position 63 zero = EOB.  Per position k the lane gets
-// (nz[k] ZRLs, main piece val[k] of len[k] bits); len 0 = nothing.
-__device__ __forceinline__ void lane_walk(const int (&c)[4], int gl, int prev, int dcd, const uint32_t* __restrict__ dctab,
-                                          const uint32_t* __restrict__ actab, uint32_t (&val)[4], int (&len)[4],
-                                          int (&nz)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int p = 4 * gl + k;
-        const bool dc = p == 0;
-        const int v = dc ? dcd : c[k];
-        const bool nzv = !dc && v != 0;
-        const bool eob = p == 63 && v == 0;
-        const int run = p - prev - 1;
-        const int cat = category_of(v);
-        const uint32_t e = dc ? dctab[cat] : actab[nzv ? (((run & 15) << 4) | cat) : 0];
-        const bool has = dc || nzv || eob;
-        val[k] = ((e & 0xFFFFu) << cat) | extra_bits(v, cat);
-        len[k] = has ? (int)(e >> 16) + cat : 0;
-        nz[k] = nzv ? (run >> 4) : 0;
-        prev = nzv ? p : prev;
-    }
-}
-
-__device__ __forceinline__ void unpack4(uint2 raw, int (&c)[4]) {
-    c[0] = (int16_t)(raw.x & 0xFFFFu);
-    c[1] = (int16_t)(raw.x >> 16);
-    c[2] = (int16_t)(raw.y & 0xFFFFu);
-    c[3] = (int16_t)(raw.y >> 16);
-}
-
-// position of the previous non-zero AC coefficient before this lane's 4 (0 = none)
-__device__ __forceinline__ int prev_nonzero(const int (&c)[4], int gl, int group) {
-    uint32_t m = (c[0] != 0 ? 1u : 0u) | (c[1] != 0 ? 2u : 0u) | (c[2] != 0 ? 4u : 0u) | (c[3] != 0 ? 8u : 0u);
-    if (gl == 0) m &= ~1u;  // position 0 is the DC, never a "previous non-zero"
-    const unsigned long long any = __ballot(m != 0);
-    const uint32_t gm = (uint32_t)(any >> (group * 16)) & 0xFFFFu;
-    const uint32_t below = gm & ((1u << gl) - 1u);
-    const int last = m ? 4 * gl + (31 - __clz((int)m)) : 0;
-    const int src = below ? (31 - __clz((int)below)) : 0;
-    const int from = __shfl(last, group * 16 + src, 64);
-    return below ? from : 0;
-}
-
-// OR `len` bits of `val` (right aligned) at bit `p` of a word image: the LDS image
-// holds MSB-first words; the global buffer holds the same words byte-swapped
-// (memory order = stream order), so the slow path swaps before its atomic OR.
-__device__ __forceinline__ void put_bits(uint32_t* __restrict__ words, unsigned long long p, uint32_t val, int len,
-                                         bool lds) {
-    const int off = (int)(p & 31);
-    const unsigned long long v = (unsigned long long)val << (64 - off - len);
-    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-    const size_t wi = (size_t)(p >> 5);
-    if (hi) atomicOr(&words[wi], lds ? hi : __builtin_bswap32(hi));
-    if (lo) atomicOr(&words[wi + 1], lds ? lo : __builtin_bswap32(lo));
-}
 
 // Sum of the counters before index `i` of a two-level (super, item) counter set,
 // by one wave: supers [0, i/kSuper) + items [kSuper*(i/kSuper), i).
@@ -106,6 +44,102 @@ __device__ __forceinline__ unsigned long long prefix_two_level(const unsigned lo
     return wave_sum_u64(acc);
 }
 
+static_assert(kChunkBlocks == 256, "one thread per block, one workgroup per chunk");
+
+// One thread walks one block (64 zigzag coefficients held in 32 registers) in
+// stream order (encoder.rs:356-404; categorize.rs:132-169): DC code + extra bits,
+// then for each non-zero AC coefficient (run >> 4) ZRL codes and
+// code((run & 15) << 4 | cat) + extra bits, EOB after trailing zeros.  The walk is
+// fully unrolled so every coefficient access is a register.  Sink receives every
+// piece (value right aligned, length in bits) in order.
+struct BlockCoef {
+    uint32_t w[32];  // coefficient 2i in the low half of w[i], 2i+1 in the high half
+};
+
+__device__ __forceinline__ void load_block(const int16_t* __restrict__ p, BlockCoef& b) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 v = q[i];
+        b.w[4 * i] = v.x;
+        b.w[4 * i + 1] = v.y;
+        b.w[4 * i + 2] = v.z;
+        b.w[4 * i + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ int coef_at(const BlockCoef& b, int k) {
+    return (k & 1) ? ((int)b.w[k >> 1] >> 16) : (int)(int16_t)(b.w[k >> 1] & 0xFFFFu);
+}
+
+template <typename Sink>
+__device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const uint32_t* __restrict__ dctab,
+                                           const uint32_t* __restrict__ actab, Sink& sink) {
+    {
+        const int cat = category_of(dcd);
+        const uint32_t e = dctab[cat];
+        sink(((e & 0xFFFFu) << cat) | extra_bits(dcd, cat), (int)(e >> 16) + cat);
+    }
+    const uint32_t z = actab[0xF0];
+    int run = 0;
+#pragma unroll
+    for (int k = 1; k < 64; ++k) {
+        const int v = coef_at(b, k);
+        if (v != 0) {
+            for (int r = run >> 4; r > 0; --r) sink(z & 0xFFFFu, (int)(z >> 16));
+            const int cat = category_of(v);
+            const uint32_t e = actab[((run & 15) << 4) | cat];
+            sink(((e & 0xFFFFu) << cat) | extra_bits(v, cat), (int)(e >> 16) + cat);
+            run = 0;
+        } else {
+            ++run;
+        }
+    }
+    if (run) {
+        const uint32_t e = actab[0];  // EOB
+        sink(e & 0xFFFFu, (int)(e >> 16));
+    }
+}
+
+struct CountSink {
+    uint32_t n = 0;
+    __device__ __forceinline__ void operator()(uint32_t, int len) { n += (uint32_t)len; }
+};
+
+// Appends pieces MSB-first into a word image: words wholly inside the block are
+// stored plainly, the first and last (shared with the neighbouring blocks) are
+// ORed atomically.  LDS image = MSB-first words; global image (slow path) =
+// byte-swapped words (memory order = stream order).
+struct EmitSink {
+    uint32_t* img;
+    bool lds;
+    unsigned long long acc;
+    int nacc;     // bits pending in acc
+    size_t w;     // next word index
+    bool first;
+    __device__ __forceinline__ void put(uint32_t word, bool shared) {
+        const uint32_t v = lds ? word : __builtin_bswap32(word);
+        if (shared)
+            atomicOr(&img[w], v);
+        else
+            img[w] = v;
+    }
+    __device__ __forceinline__ void operator()(uint32_t val, int len) {
+        acc = (acc << len) | val;
+        nacc += len;
+        if (nacc >= 32) {
+            nacc -= 32;
+            put((uint32_t)(acc >> nacc), first);
+            first = false;
+            ++w;
+            acc &= (1ull << nacc) - 1ull;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if (nacc > 0) put((uint32_t)(acc << (32 - nacc)), true);
+    }
+};
+
 // ---------------------------------------------------------------------- k_bits
 __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, const int16_t* __restrict__ dcdiff,
                                               const uint32_t* __restrict__ code_tab, Geom g,
@@ -114,54 +148,31 @@ __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, 
     __shared__ uint32_t sTab[4 * 256];
     __shared__ uint32_t sWave[4];
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int group = lane >> 4, gl = lane & 15;
     const int frame = blockIdx.y;
     const unsigned chunk = blockIdx.x;
     const long long el0 = (long long)chunk * kChunkBlocks;
     const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
-    const long long base = (long long)frame * g.bpf + el0;
+    const long long e = (long long)frame * g.bpf + el0 + tid;
     for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
-
-    // this wave's 16 blocks: all loads in flight before the tables are needed
-    uint2 raw[4];
-    int dcd[4];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int b = wave * 16 + it * 4 + group;
-        const bool valid = b < nb;
-        raw[it] = valid ? *reinterpret_cast<const uint2*>(coef + (base + b) * 64 + 4 * gl) : make_uint2(0, 0);
-        dcd[it] = (valid && gl == 0) ? (int)dcdiff[base + b] : 0;
+    const bool valid = tid < nb;
+    BlockCoef b;
+    int dcd = 0;
+    if (valid) {
+        load_block(coef + e * 64, b);
+        dcd = dcdiff[e];
     }
     __syncthreads();
-    uint32_t acc = 0;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int b = wave * 16 + it * 4 + group;
-        const bool valid = b < nb;
-        int c[4];
-        unpack4(raw[it], c);
-        const int prev = prev_nonzero(c, gl, group);
-        const int k = (int)((el0 + b) % g.bpm);
+    uint32_t bits = 0;
+    if (valid) {
+        const int k = ((int)(el0 % g.bpm) + tid) % g.bpm;
         const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
-        const uint32_t zl = tb[256 + 0xF0] >> 16;
-        uint32_t val[4];
-        int len[4], nz[4];
-        lane_walk(c, gl, prev, dcd[it], tb, tb + 256, val, len, nz);
-        uint32_t nbits = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) nbits += (uint32_t)nz[j] * zl + (uint32_t)len[j];
-        nbits = valid ? nbits : 0u;
-        nbits += __shfl_xor(nbits, 8, 16);
-        nbits += __shfl_xor(nbits, 4, 16);
-        nbits += __shfl_xor(nbits, 2, 16);
-        nbits += __shfl_xor(nbits, 1, 16);
-        if (gl == 0 && valid) block_bits[base + b] = (uint16_t)nbits;
-        acc += nbits;
+        CountSink cs;
+        walk_block(b, dcd, tb, tb + 256, cs);
+        bits = cs.n;
+        block_bits[e] = (uint16_t)bits;
     }
-    // every lane of a group holds its group's block sum: count it once per group
-    acc = (gl == 0) ? acc : 0u;
-    acc = wave_sum_u32(acc);
-    if (lane == 0) sWave[wave] = acc;
+    const uint32_t ws = wave_sum_u32(bits);
+    if (lane == 0) sWave[wave] = ws;
     __syncthreads();
     if (tid == 0) {
         const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
@@ -171,11 +182,11 @@ __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, 
 }
 
 // --------------------------------------------------------------------- k_place
-// LDS word image capacity of one chunk: 32 Ki bits = 512 bits per block on
+// LDS word image capacity of one chunk: 128 Ki bits = 512 bits per block on
 // average (the 4K q90 workload averages ~110).  A chunk that needs more (worst
-// case kMaxBlockBits per block) is placed straight into the zeroed global buffer
-// with atomic ORs instead: slower, same bytes.
-constexpr int kPackWords = 1024;
+// case kMaxBlockBits per block) writes straight into the zeroed global buffer
+// instead: slower, same bytes.
+constexpr int kPackWords = 4096;
 
 __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef, const int16_t* __restrict__ dcdiff,
                                                const uint32_t* __restrict__ code_tab, Geom g,
@@ -186,43 +197,38 @@ __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef,
                                                uint32_t* __restrict__ packed, int* __restrict__ status) {
     __shared__ uint32_t sW[kPackWords + 2];
     __shared__ uint32_t sTab[4 * 256];
-    __shared__ uint32_t sOff[kChunkBlocks];
-    __shared__ uint32_t sTotal;
+    __shared__ uint32_t sWave[4];
     __shared__ unsigned long long sBase;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int group = lane >> 4, gl = lane & 15;
     const int frame = blockIdx.y;
     const unsigned chunk = blockIdx.x;
     const long long el0 = (long long)chunk * kChunkBlocks;
     const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
-    const long long base = (long long)frame * g.bpf + el0;
+    const long long e = (long long)frame * g.bpf + el0 + tid;
     for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
-
-    uint2 raw[4];
-    int dcd[4];
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int b = wave * 16 + it * 4 + group;
-        const bool valid = b < nb;
-        raw[it] = valid ? *reinterpret_cast<const uint2*>(coef + (base + b) * 64 + 4 * gl) : make_uint2(0, 0);
-        dcd[it] = (valid && gl == 0) ? (int)dcdiff[base + b] : 0;
+    const bool valid = tid < nb;
+    BlockCoef b;
+    int dcd = 0;
+    uint32_t mine = 0;
+    if (valid) {
+        load_block(coef + e * 64, b);
+        dcd = dcdiff[e];
+        mine = block_bits[e];
     }
-    if (wave == 0) {  // chunk offset (two-level sums) and block offsets within the chunk
+    // block offsets within the chunk: workgroup scan of the block bit counts
+    const uint32_t incl = wave_incl_scan_u32(mine);
+    if (lane == 63) sWave[wave] = incl;
+    if (wave == 0) {
         const unsigned long long pre =
             prefix_two_level(super_bits + (size_t)frame * g.nsuper, chunk_bits + (size_t)frame * g.nch, chunk);
-        const uint32_t v = lane < nb ? (uint32_t)block_bits[base + lane] : 0u;
-        const uint32_t incl = wave_incl_scan_u32(v);
-        const uint32_t total = __shfl(incl, 63, 64);
-        sOff[lane] = incl - v;
-        if (lane == 0) {
-            sBase = pre;
-            sTotal = total;
-            if (chunk == (unsigned)g.nch - 1) total_bits[frame] = pre + total;
-        }
+        if (lane == 0) sBase = pre;
     }
     __syncthreads();
+    uint32_t wpre = 0;
+    for (int w = 0; w < wave; ++w) wpre += sWave[w];
+    const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
     const unsigned long long bit0 = sBase;
-    const uint32_t total = sTotal;
+    if (tid == 0 && chunk == (unsigned)g.nch - 1) total_bits[frame] = bit0 + total;
     const int shift = (int)(bit0 & 31);
     const int nw = (int)((shift + (unsigned long long)total + 31) >> 5);
     if (((bit0 + total + 31) >> 5) + 1 > (unsigned long long)g.packed_words) {
@@ -231,53 +237,19 @@ __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef,
     }
     uint32_t* const pk = packed + (size_t)frame * g.packed_words + (bit0 >> 5);
     const bool in_lds = nw + 1 <= kPackWords + 2;
-    uint32_t* const img = in_lds ? sW : pk;  // slow path: OR into the zeroed global buffer
     if (in_lds)
         for (int i = tid; i < nw + 1; i += 256) sW[i] = 0u;
     __syncthreads();
-
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-        const int b = wave * 16 + it * 4 + group;
-        const bool valid = b < nb;
-        int c[4];
-        unpack4(raw[it], c);
-        const int prev = prev_nonzero(c, gl, group);
-        const int k = (int)((el0 + b) % g.bpm);
+    if (valid) {
+        const int k = ((int)(el0 % g.bpm) + tid) % g.bpm;
         const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
-        const uint32_t z = tb[256 + 0xF0];
-        const uint32_t zc = z & 0xFFFFu;
-        const int zl = (int)(z >> 16);
-        uint32_t val[4];
-        int len[4], nz[4];
-        lane_walk(c, gl, prev, dcd[it], tb, tb + 256, val, len, nz);
-        uint32_t mine = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mine += (uint32_t)nz[j] * (uint32_t)zl + (uint32_t)len[j];
-        mine = valid ? mine : 0u;
-        uint32_t incl = mine;  // inclusive scan over the 16 lanes of the block
-#pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
-            const uint32_t t = __shfl_up(incl, d, 16);
-            if (gl >= d) incl += t;
-        }
-        if (valid) {
-            unsigned long long pos = (unsigned long long)sOff[b] + (unsigned)shift + (incl - mine);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                for (int r = 0; r < nz[j]; ++r) {
-                    put_bits(img, pos, zc, zl, in_lds);
-                    pos += (unsigned)zl;
-                }
-                if (len[j]) {
-                    put_bits(img, pos, val[j], len[j], in_lds);
-                    pos += (unsigned)len[j];
-                }
-            }
-        }
+        const uint32_t start = (uint32_t)shift + wpre + incl - mine;  // bit position in the image
+        EmitSink es{in_lds ? sW : pk, in_lds, 0ull, (int)(start & 31), (size_t)(start >> 5), true};
+        walk_block(b, dcd, tb, tb + 256, es);
+        es.finish();
     }
     __syncthreads();
-    if (in_lds) {  // interior words plain, the two edge words ORed (shared with neighbours)
+    if (in_lds) {  // interior words plain, the two edge words ORed (shared with neighbouring chunks)
         for (int i = tid; i < nw; i += 256) {
             const uint32_t v = __builtin_bswap32(sW[i]);
             if (i == 0 || i == nw - 1)

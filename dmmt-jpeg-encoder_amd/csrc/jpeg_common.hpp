@@ -15,7 +15,7 @@ static constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 
 // histograms into replica (blockIdx.x % kHistReps) to spread atomic traffic.
 static constexpr int kHistReps = 16;
 // Blocks per entropy chunk (k_bits / k_place): one workgroup each.
-static constexpr int kChunkBlocks = 64;
+static constexpr int kChunkBlocks = 256;
 // Worst-case entropy-coded bits of one block: DC code 16 + 12 extra bits, 63 AC
 // tokens of code 16 + 12 extra bits (|coef| <= 2048 for 8-bit-range input).
 static constexpr int kMaxBlockBits = 28 * 64;
