@@ -33,6 +33,16 @@ struct EventPair {
     hipEvent_t a, b;
 };
 
+// One instantiated capture of the whole per-call pipeline.  The key holds every
+// value baked into the launches (pointers, geometry, stream), so a hit replays
+// exactly the launches a direct enqueue would make.
+struct GraphEntry {
+    std::vector<uint64_t> key;
+    hipGraphExec_t exec = nullptr;
+    uint64_t last_use = 0;
+};
+constexpr size_t kMaxGraphs = 16;
+
 }  // namespace
 
 struct dmmt_ctx {
@@ -55,6 +65,10 @@ struct dmmt_ctx {
     std::vector<hipEvent_t> free_events;
     double stage_ms[ST_COUNT] = {0};
     int stage_launches[ST_COUNT] = {0};
+    // replayed pipelines (opt-in: DMMT_GRAPHS=1; measured no faster than direct launches on 4K frames)
+    bool use_graphs = false;
+    std::vector<GraphEntry> graphs;
+    uint64_t graph_clock = 0;
 };
 
 namespace {
@@ -271,16 +285,69 @@ int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bit
     return DMMT_OK;
 }
 
+int enqueue_direct(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, int nf, const Geom& g,
+                   const Work& w, int bits, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st) {
+    {
+        StageTimer t(c, ST_FRONT, st);
+        HIP_TRY(launch_front(d_rgb, frame_stride, sb, nf, g, w, st));
+    }
+    return enqueue_back_half(c, g, nf, w, bits, out, out_stride, out_len, st);
+}
+
+void destroy_graphs(dmmt_ctx* c) {
+    for (auto& e : c->graphs) (void)hipGraphExecDestroy(e.exec);
+    c->graphs.clear();
+}
+
+// The seven launches of one call cost ~8-10 us of dispatch gap each when issued
+// one by one; replaying them as one instantiated graph removes most of that.
+// Stage profiling needs per-kernel events, so it always launches directly.
 int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, int nf, const Geom& g,
                    const dmmt_options* opt, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st) {
     Work w;
     int rc;
     if ((rc = prepare(c, g, nf, opt, sb, st, &w))) return rc;
-    {
-        StageTimer t(c, ST_FRONT, st);
-        HIP_TRY(launch_front(d_rgb, frame_stride, sb, nf, g, w, st));
+    const int bits = opt->bits_per_channel;
+    if (!c->use_graphs || c->profile)
+        return enqueue_direct(c, d_rgb, frame_stride, sb, nf, g, w, bits, out, out_stride, out_len, st);
+    std::vector<uint64_t> key = {(uint64_t)(uintptr_t)d_rgb, (uint64_t)frame_stride, (uint64_t)sb, (uint64_t)nf,
+                                 (uint64_t)g.width, (uint64_t)g.height, (uint64_t)g.hr, (uint64_t)g.vr,
+                                 (uint64_t)g.maxval, (uint64_t)g.restart_interval, (uint64_t)bits,
+                                 (uint64_t)(uintptr_t)out, (uint64_t)out_stride, (uint64_t)(uintptr_t)out_len,
+                                 (uint64_t)(uintptr_t)st};
+    const void* const* wp = reinterpret_cast<const void* const*>(&w);
+    static_assert(sizeof(Work) % sizeof(void*) == 0, "Work holds pointers only");
+    for (size_t i = 0; i < sizeof(Work) / sizeof(void*); ++i) key.push_back((uint64_t)(uintptr_t)wp[i]);
+    GraphEntry* hit = nullptr;
+    for (auto& e : c->graphs)
+        if (e.key == key) hit = &e;
+    if (!hit) {
+        hipGraph_t graph = nullptr;
+        HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        rc = enqueue_direct(c, d_rgb, frame_stride, sb, nf, g, w, bits, out, out_stride, out_len, st);
+        hipError_t e = hipStreamEndCapture(st, &graph);
+        if (rc) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
+        HIP_TRY(e);
+        hipGraphExec_t exec = nullptr;
+        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        HIP_TRY(e);
+        if (c->graphs.size() >= kMaxGraphs) {  // evict the least recently used
+            size_t lru = 0;
+            for (size_t i = 1; i < c->graphs.size(); ++i)
+                if (c->graphs[i].last_use < c->graphs[lru].last_use) lru = i;
+            (void)hipGraphExecDestroy(c->graphs[lru].exec);
+            c->graphs.erase(c->graphs.begin() + lru);
+        }
+        c->graphs.push_back({std::move(key), exec, 0});
+        hit = &c->graphs.back();
     }
-    return enqueue_back_half(c, g, nf, w, opt->bits_per_channel, out, out_stride, out_len, st);
+    hit->last_use = ++c->graph_clock;
+    HIP_TRY(hipGraphLaunch(hit->exec, st));
+    return DMMT_OK;
 }
 
 // read and clear the device status word
@@ -326,6 +393,7 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return DMMT_E_NO_DEVICE;
     dmmt_ctx* c = new dmmt_ctx();
     c->device = device;
+    if (const char* e = getenv("DMMT_GRAPHS")) c->use_graphs = atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return DMMT_E_HIP;
@@ -339,6 +407,7 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     drain_events(c);
+    destroy_graphs(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
     DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff,     &c->ac_hist,    &c->dc_hist,
                       &c->code_tab,   &c->hdr_len,    &c->total_bits, &c->packed,     &c->block_bits,

@@ -31,6 +31,10 @@
 
 namespace dmmt {
 
+#ifdef DMMT_PHASE_TRACE
+static __device__ unsigned long long g_trace[64];
+#endif
+
 // Sum of the counters before index `i` of a two-level (super, item) counter set,
 // by one wave: supers [0, i/kSuper) + items [kSuper*(i/kSuper), i).
 template <typename T>
@@ -147,6 +151,7 @@ __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, 
                                               unsigned long long* __restrict__ super_bits) {
     __shared__ uint32_t sTab[4 * 256];
     __shared__ uint32_t sWave[4];
+    DMMT_TRACE_START;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
     const unsigned chunk = blockIdx.x;
@@ -162,6 +167,7 @@ __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, 
         dcd = dcdiff[e];
     }
     __syncthreads();
+    DMMT_TRACE(0);
     uint32_t bits = 0;
     if (valid) {
         const int k = ((int)(el0 % g.bpm) + tid) % g.bpm;
@@ -179,6 +185,8 @@ __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, 
         chunk_bits[(size_t)frame * g.nch + chunk] = total;
         atomicAdd(&super_bits[(size_t)frame * g.nsuper + chunk / kSuper], (unsigned long long)total);
     }
+    DMMT_TRACE(1);
+    DMMT_TRACE_FLUSH(0);
 }
 
 // --------------------------------------------------------------------- k_place
@@ -199,6 +207,7 @@ __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef,
     __shared__ uint32_t sTab[4 * 256];
     __shared__ uint32_t sWave[4];
     __shared__ unsigned long long sBase;
+    DMMT_TRACE_START;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
     const unsigned chunk = blockIdx.x;
@@ -224,6 +233,7 @@ __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef,
         if (lane == 0) sBase = pre;
     }
     __syncthreads();
+    DMMT_TRACE(4);
     uint32_t wpre = 0;
     for (int w = 0; w < wave; ++w) wpre += sWave[w];
     const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
@@ -240,6 +250,7 @@ __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef,
     if (in_lds)
         for (int i = tid; i < nw + 1; i += 256) sW[i] = 0u;
     __syncthreads();
+    DMMT_TRACE(5);
     if (valid) {
         const int k = ((int)(el0 % g.bpm) + tid) % g.bpm;
         const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
@@ -249,6 +260,7 @@ __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef,
         es.finish();
     }
     __syncthreads();
+    DMMT_TRACE(6);
     if (in_lds) {  // interior words plain, the two edge words ORed (shared with neighbouring chunks)
         for (int i = tid; i < nw; i += 256) {
             const uint32_t v = __builtin_bswap32(sW[i]);
@@ -258,6 +270,8 @@ __global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef,
                 pk[i] = v;
         }
     }
+    DMMT_TRACE(7);
+    DMMT_TRACE_FLUSH(0);
 }
 
 // ------------------------------------------------------------------- stuffing
@@ -438,3 +452,11 @@ hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t
 }
 
 }  // namespace dmmt
+
+#ifdef DMMT_PHASE_TRACE
+extern "C" int dmmt_debug_trace_entropy(unsigned long long* out64) {
+    if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(dmmt::g_trace), 64 * 8) != hipSuccess) return -1;
+    unsigned long long z[64] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(dmmt::g_trace), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -32,6 +32,10 @@
 
 namespace dmmt {
 
+#ifdef DMMT_PHASE_TRACE
+static __device__ unsigned long long g_trace[64];
+#endif
+
 __constant__ uint8_t c_zigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                                      12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                                      35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
@@ -101,6 +105,74 @@ __device__ __forceinline__ void rgb_to_ycbcr(float r, float g, float b, float& y
 //  E  AC symbols: one wave per block, lane = zigzag position, ballot finds the
 //     previous non-zero coefficient; LDS histogram, flushed once per workgroup.
 
+// Raw pixel staging: a tile row is 256 pixels = RB bytes, fetched as the RC
+// aligned 16-byte chunks that cover it at any alignment (byte loads only for a
+// chunk that crosses the frame's first or last byte).  Chunk q of a tile is
+// chunk q % RC of tile row q / RC; thread t owns chunks t, t+256, ...  In LDS a
+// tile row starts at row * RS, its first pixel `misalign` bytes further.
+template <typename Sample, int ROWS>
+struct RawTile {
+    static constexpr int RB = 256 * 3 * (int)sizeof(Sample);
+    static constexpr int RC = RB / 16 + 1;
+    static constexpr int RS = RC * 16;
+    static constexpr int NCHUNK = ROWS * RC;
+    static constexpr int NQ = (NCHUNK + 255) / 256;
+    static constexpr int BYTES = NCHUNK * 16;
+
+    __device__ static __forceinline__ long long row_start(const Geom& g, int x0, int py) {
+        return ((long long)py * g.width + x0) * 3 * (long long)sizeof(Sample);
+    }
+    __device__ static __forceinline__ int misalign(const uint8_t* fbase, long long start) {
+        return (int)(((uintptr_t)fbase + (uintptr_t)start) & 15u);
+    }
+
+    __device__ static __forceinline__ void load(const uint8_t* __restrict__ fbase, long long fbytes, const Geom& g,
+                                                int x0, int y0, int tid, uint4 (&v)[NQ]) {
+        const long long rowbytes = (long long)min(256, g.width - x0) * 3 * (long long)sizeof(Sample);
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            v[i] = make_uint4(0u, 0u, 0u, 0u);
+            const int q = tid + 256 * i;
+            const int row = q / RC, j = q - (q / RC) * RC;
+            const int py = y0 + row;
+            if (q >= NCHUNK || py >= g.height) continue;
+            const long long start = row_start(g, x0, py);
+            const long long c = start - misalign(fbase, start) + 16LL * j;  // frame-relative
+            if (c >= start + rowbytes) continue;
+            if (c >= 0 && c + 16 <= fbytes) {
+                v[i] = *reinterpret_cast<const uint4*>(fbase + c);
+            } else {
+                uint32_t w[4] = {0u, 0u, 0u, 0u};
+                for (int k = 0; k < 16; ++k)
+                    if (c + k >= 0 && c + k < fbytes) w[k >> 2] |= (uint32_t)fbase[c + k] << (8 * (k & 3));
+                v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    }
+
+    __device__ static __forceinline__ void stage(uint8_t* sRaw, int tid, const uint4 (&v)[NQ]) {
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            const int q = tid + 256 * i;
+            if (q < NCHUNK) reinterpret_cast<uint4*>(sRaw)[q] = v[i];
+        }
+    }
+};
+
+// One workgroup (256 threads) per tile = TM horizontally adjacent MCUs of one
+// MCU row (256 padded pixel columns, 8*VR rows), looping over the frame's tiles
+// (grid = resident workgroups; blockIdx.y = frame) with the next tile's pixels
+// prefetched into registers while the current one computes.
+//  A  colour + subsampling + row DCT, fused: one thread per (chroma row, chroma
+//     block) converts its 8*HR x VR pixels (raw bytes from LDS), box-averages the
+//     chroma in the reference's sum order and runs the row pass of the HR*VR luma
+//     rows and the two chroma rows in registers -> block-major LDS (stride BS)
+//  C  column DCT + quantise: one lane per (block, column); results held in
+//     registers across a barrier, then scattered in zigzag order into the
+//     (aliased) int16 block image in local MCU emission order
+//  D  coalesced 16-byte stores of the tile's blocks + DC values
+//  E  AC symbols: one wave per block, lane = zigzag position, ballot finds the
+//     previous non-zero coefficient; LDS histogram, flushed once per workgroup.
 template <int HR, int VR, typename Sample>
 __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, size_t frame_stride, Geom g,
                                                const float* __restrict__ norm_lut,
@@ -108,149 +180,209 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
                                                int16_t* __restrict__ coef, int16_t* __restrict__ dc,
                                                uint32_t* __restrict__ ac_hist,  // [frames][reps][2][256]
                                                int* __restrict__ status) {
-    constexpr int TM = 32 / HR;
-    constexpr int ROWS = 8 * VR;
+    constexpr int TM = 32 / HR;      // MCUs per tile
+    constexpr int ROWS = 8 * VR;     // pixel rows per tile
     constexpr int NLUMA = HR * VR;
     constexpr int BPM = NLUMA + 2;
-    constexpr int NB = TM * BPM;
-    constexpr int NYB = 32 * VR;   // Y blocks in the tile
-    constexpr int CW = 256 / HR;   // chroma samples per tile row
-    constexpr int CB = CW / 8;     // chroma blocks per component
-    constexpr int YS = 256 + 4;    // padded LDS row strides (floats)
-    constexpr int CS = CW + 4;
-    constexpr int NGROUP = (ROWS / VR) * CW;  // subsampling groups per tile
+    constexpr int NB = TM * BPM;     // blocks per tile
+    constexpr int NYB = 32 * VR;     // Y blocks: 32 columns x VR rows
+    constexpr int CB = TM;           // chroma blocks per component
+    constexpr int BS = 72;           // LDS floats per block: 64 + pad (conflict-free column reads)
+    constexpr int NJ = 8 * CB;       // fused jobs (chroma row, chroma block)
+    constexpr int SB = (int)sizeof(Sample);
+    constexpr int PXB = 8 * HR * 3 * SB;  // raw bytes of one job row
+    constexpr int PXW = PXB / 4;
+    constexpr int NCJ = NB * 8;      // column jobs
+    constexpr int JPT = (NCJ + 255) / 256;
+    using Raw = RawTile<Sample, ROWS>;
 
-    __shared__ float sY[ROWS * YS];
-    __shared__ float sCb[8 * CS];
-    __shared__ float sCr[8 * CS];
-    __shared__ __attribute__((aligned(16))) int16_t sCoef[NB * 64];
+    // row-transformed blocks (A..C), then the quantised int16 blocks (C..E)
+    __shared__ __attribute__((aligned(16))) float sT[NB * BS];
+    __shared__ __attribute__((aligned(16))) uint8_t sRaw[Raw::BYTES];
     __shared__ uint32_t sHist[2 * 256];
     __shared__ float sLut[256];
     __shared__ float sQ[128];
+    int16_t* const sCoef = reinterpret_cast<int16_t*>(sT);
 
+    DMMT_TRACE_START;
     const int tid = threadIdx.x;
     const int frame = blockIdx.y;
-    const Sample* img = rgb + (size_t)frame * frame_stride;
+    const uint8_t* fbase = reinterpret_cast<const uint8_t*>(rgb + (size_t)frame * frame_stride);
+    const long long fbytes = (long long)g.width * g.height * 3 * SB;
     for (int i = tid; i < 512; i += 256) sHist[i] = 0;
     if (tid < 128) sQ[tid] = qtab[tid];
-    if (sizeof(Sample) == 1) sLut[tid] = norm_lut[tid];
-    __syncthreads();
+    if (SB == 1) sLut[tid] = norm_lut[tid];
+    // the column pass always handles column tid & 7: its 8 zigzag destinations
+    uint8_t zz[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) zz[r] = c_inv_zigzag[r * 8 + (tid & 7)];
 
     const int tiles_per_row = (g.mcux + TM - 1) / TM;
     const int ntiles = tiles_per_row * g.mcuy;
     int bad = 0;
 
+    uint4 raw[Raw::NQ];
+    if ((int)blockIdx.x < ntiles) {
+        const int my = blockIdx.x / tiles_per_row;
+        Raw::load(fbase, fbytes, g, (blockIdx.x - my * tiles_per_row) * TM * 8 * HR, my * ROWS, tid, raw);
+    }
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int my = tile / tiles_per_row;
         const int mx0 = (tile - my * tiles_per_row) * TM;
         const int x0 = mx0 * 8 * HR;
         const int y0 = my * ROWS;
 
-        // ---- A: color conversion + subsampling (padder.rs: outside = black)
-        for (int grp = tid; grp < NGROUP; grp += 256) {
-            const int gc = grp % CW;
-            const int gr = grp / CW;
-            float cbs = 0.0f, crs = 0.0f;
+        Raw::stage(sRaw, tid, raw);
+        __syncthreads();
+        {  // prefetch the next tile's pixels; they land while this tile computes
+            const int nt = tile + gridDim.x;
+            if (nt < ntiles) {
+                const int ny = nt / tiles_per_row;
+                Raw::load(fbase, fbytes, g, (nt - ny * tiles_per_row) * TM * 8 * HR, ny * ROWS, tid, raw);
+            }
+        }
+
+        // ---- A: colour + subsampling + row pass (color.rs:75-100, padder.rs: outside
+        //      = black, subsampling.rs Subsampler::rect x outer / y inner, arai.rs:97-99)
+        if (tid < NJ) {
+            const int c = tid % CB, r = tid / CB;  // chroma block, chroma row
+            const int lx0 = c * 8 * HR;            // first pixel column of the job
+            uint32_t pw[VR][PXW];                  // raw bytes of the job's VR pixel rows
 #pragma unroll
-            for (int dx = 0; dx < HR; ++dx) {  // Subsampler::rect: x outer, y inner
+            for (int dy = 0; dy < VR; ++dy) {
+                const int ly = r * VR + dy;
+                const long long start = Raw::row_start(g, x0, y0 + ly);
+                const int mis = Raw::misalign(fbase, start);
+                const uint8_t* src = sRaw + ly * Raw::RS + mis + lx0 * 3 * SB;
+                if ((mis & 7) == 0) {
 #pragma unroll
-                for (int dy = 0; dy < VR; ++dy) {
-                    const int px = x0 + gc * HR + dx;
-                    const int py = y0 + gr * VR + dy;
-                    float r = 0.0f, gg = 0.0f, b = 0.0f;
-                    if (px < g.width && py < g.height) {
-                        const Sample* p = img + ((size_t)py * g.width + px) * 3;
-                        const uint32_t ir = p[0], ig = p[1], ib = p[2];
-                        bad |= (int)(ir > (uint32_t)g.maxval) | (int)(ig > (uint32_t)g.maxval) |
-                               (int)(ib > (uint32_t)g.maxval);
-                        if (sizeof(Sample) == 1) {
-                            r = sLut[ir];
-                            gg = sLut[ig];
-                            b = sLut[ib];
-                        } else {
-                            r = norm_lut[ir];
-                            gg = norm_lut[ig];
-                            b = norm_lut[ib];
-                        }
+                    for (int k = 0; k < PXW / 2; ++k) {
+                        const uint2 u = reinterpret_cast<const uint2*>(src)[k];
+                        pw[dy][2 * k] = u.x;
+                        pw[dy][2 * k + 1] = u.y;
                     }
-                    float y, cb, cr;
-                    rgb_to_ycbcr(r, gg, b, y, cb, cr);
-                    sY[(gr * VR + dy) * YS + gc * HR + dx] = y;
-                    if (dx == 0 && dy == 0) {
-                        cbs = cb;
-                        crs = cr;
-                    } else {
-                        cbs = cbs + cb;
-                        crs = crs + cr;
-                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < PXW; ++k)
+                        pw[dy][k] = (uint32_t)src[4 * k] | ((uint32_t)src[4 * k + 1] << 8) |
+                                    ((uint32_t)src[4 * k + 2] << 16) | ((uint32_t)src[4 * k + 3] << 24);
                 }
             }
-            if (HR * VR > 1) {  // average() divides by the sample count
-                cbs = cbs / (float)(HR * VR);
-                crs = crs / (float)(HR * VR);
+            float yv[VR][HR][8];
+            float cbv[8], crv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {  // chroma sample k of the row
+                float cbs = 0.0f, crs = 0.0f;
+#pragma unroll
+                for (int dx = 0; dx < HR; ++dx) {
+#pragma unroll
+                    for (int dy = 0; dy < VR; ++dy) {
+                        const int jx = k * HR + dx;  // pixel within the job row
+                        const int px = x0 + lx0 + jx;
+                        const int py = y0 + r * VR + dy;
+                        float rr = 0.0f, gg = 0.0f, bb = 0.0f;
+                        if (px < g.width && py < g.height) {
+                            uint32_t sv[3];
+#pragma unroll
+                            for (int ch = 0; ch < 3; ++ch) {
+                                const int si = jx * 3 + ch;  // sample index in the row
+                                sv[ch] = SB == 1 ? (pw[dy][si >> 2] >> (8 * (si & 3))) & 0xFFu
+                                                 : (pw[dy][si >> 1] >> (16 * (si & 1))) & 0xFFFFu;
+                            }
+                            bad |= (int)(sv[0] > (uint32_t)g.maxval) | (int)(sv[1] > (uint32_t)g.maxval) |
+                                   (int)(sv[2] > (uint32_t)g.maxval);
+                            if (SB == 1) {
+                                rr = sLut[sv[0]];
+                                gg = sLut[sv[1]];
+                                bb = sLut[sv[2]];
+                            } else {
+                                rr = norm_lut[sv[0]];
+                                gg = norm_lut[sv[1]];
+                                bb = norm_lut[sv[2]];
+                            }
+                        }
+                        float y, cb, cr;
+                        rgb_to_ycbcr(rr, gg, bb, y, cb, cr);
+                        yv[dy][jx >> 3][jx & 7] = y;
+                        if (dx == 0 && dy == 0) {
+                            cbs = cb;
+                            crs = cr;
+                        } else {
+                            cbs = cbs + cb;
+                            crs = crs + cr;
+                        }
+                    }
+                }
+                if (HR * VR > 1) {  // average() divides by the sample count
+                    cbs = cbs / (float)(HR * VR);
+                    crs = crs / (float)(HR * VR);
+                }
+                cbv[k] = cbs;
+                crv[k] = crs;
             }
-            sCb[gr * CS + gc] = cbs;
-            sCr[gr * CS + gc] = crs;
+#pragma unroll
+            for (int dy = 0; dy < VR; ++dy) {
+                const int ly = r * VR + dy;
+#pragma unroll
+                for (int jb = 0; jb < HR; ++jb) {
+                    arai8(yv[dy][jb]);
+                    float4* o = reinterpret_cast<float4*>(sT + ((ly >> 3) * 32 + c * HR + jb) * BS + (ly & 7) * 8);
+                    o[0] = make_float4(yv[dy][jb][0], yv[dy][jb][1], yv[dy][jb][2], yv[dy][jb][3]);
+                    o[1] = make_float4(yv[dy][jb][4], yv[dy][jb][5], yv[dy][jb][6], yv[dy][jb][7]);
+                }
+            }
+            arai8(cbv);
+            arai8(crv);
+            float4* ob = reinterpret_cast<float4*>(sT + (NYB + c) * BS + r * 8);
+            ob[0] = make_float4(cbv[0], cbv[1], cbv[2], cbv[3]);
+            ob[1] = make_float4(cbv[4], cbv[5], cbv[6], cbv[7]);
+            float4* orr = reinterpret_cast<float4*>(sT + (NYB + CB + c) * BS + r * 8);
+            orr[0] = make_float4(crv[0], crv[1], crv[2], crv[3]);
+            orr[1] = make_float4(crv[4], crv[5], crv[6], crv[7]);
         }
         __syncthreads();
+        DMMT_TRACE(0);
 
-        // ---- B: row pass (stride 1), arai.rs:97-99
-        for (int job = tid; job < NB * 8; job += 256) {
-            const int row = job & 7;
-            const int blk = job >> 3;
-            float* p;
-            if (blk < NYB)
-                p = sY + ((blk / 32) * 8 + row) * YS + (blk % 32) * 8;
-            else if (blk < NYB + CB)
-                p = sCb + row * CS + (blk - NYB) * 8;
-            else
-                p = sCr + row * CS + (blk - NYB - CB) * 8;
-            float v[8];
+        // ---- C: column pass (stride 8, arai.rs:100-102), quantise (quantizer.rs:53-62)
+        uint32_t qv[JPT][4];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = p[i];
-            arai8(v);
+        for (int jj = 0; jj < JPT; ++jj) {
+            const int job = tid + 256 * jj;
+            if (job < NCJ) {
+                const int col = job & 7, blk = job >> 3;
+                const float* q = sQ + (blk < NYB ? 0 : 64) + col;
+                float v[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) p[i] = v[i];
-        }
-        __syncthreads();
-
-        // ---- C: column pass (stride 8), arai.rs:100-102, then quantise
-        for (int job = tid; job < NB * 8; job += 256) {
-            const int col = job & 7;
-            const int blk = job >> 3;
-            const float* p;
-            int stride, comp, el;
-            if (blk < NYB) {
-                const int by = blk / 32, bx = blk % 32;
-                p = sY + (by * 8) * YS + bx * 8 + col;
-                stride = YS;
-                comp = 0;
-                el = (bx / HR) * BPM + by * HR + (bx % HR);  // TL,TR,BL,BR (block_entangler.rs:69-77)
-            } else if (blk < NYB + CB) {
-                const int cx = blk - NYB;
-                p = sCb + cx * 8 + col;
-                stride = CS;
-                comp = 1;
-                el = cx * BPM + NLUMA;
-            } else {
-                const int cx = blk - NYB - CB;
-                p = sCr + cx * 8 + col;
-                stride = CS;
-                comp = 1;
-                el = cx * BPM + NLUMA + 1;
+                for (int i = 0; i < 8; ++i) v[i] = sT[blk * BS + i * 8 + col];
+                arai8(v);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    qv[jj][i] = (uint32_t)(uint16_t)quantize(v[2 * i], q[16 * i]) |
+                                ((uint32_t)(uint16_t)quantize(v[2 * i + 1], q[16 * i + 8]) << 16);
             }
-            float v[8];
+        }
+        __syncthreads();  // every column read: the int16 image may now overwrite sT
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = p[i * stride];
-            arai8(v);
-            int16_t* o = sCoef + el * 64;
+        for (int jj = 0; jj < JPT; ++jj) {
+            const int job = tid + 256 * jj;
+            if (job < NCJ) {
+                const int blk = job >> 3;
+                int el;
+                if (blk < NYB) {
+                    const int by = blk / 32, bx = blk % 32;
+                    el = (bx / HR) * BPM + by * HR + (bx % HR);  // TL,TR,BL,BR (block_entangler.rs:69-77)
+                } else if (blk < NYB + CB) {
+                    el = (blk - NYB) * BPM + NLUMA;
+                } else {
+                    el = (blk - NYB - CB) * BPM + NLUMA + 1;
+                }
+                int16_t* o = sCoef + el * 64;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int nat = r * 8 + col;
-                o[c_inv_zigzag[nat]] = quantize(v[r], sQ[comp * 64 + nat]);
+                for (int i = 0; i < 8; ++i) o[zz[i]] = (int16_t)(qv[jj][i >> 1] >> (16 * (i & 1)));
             }
         }
         __syncthreads();
+        DMMT_TRACE(2);
 
         // ---- D: write the tile's blocks (contiguous in emission order) and DCs
         const int nmcu_valid = min(TM, g.mcux - mx0);
@@ -262,6 +394,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
             for (int i = tid; i < nblk * 8; i += 256) dst[i] = src[i];
             for (int b = tid; b < nblk; b += 256) dc[e0 + b] = sCoef[b * 64];
         }
+        DMMT_TRACE(3);
 
         // ---- E: AC run/size symbols (categorize.rs:132-151)
         {
@@ -281,6 +414,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
             }
         }
         __syncthreads();
+        DMMT_TRACE(4);
     }
 
     if (bad) atomicOr(status, 1);
@@ -289,6 +423,8 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
         const uint32_t v = sHist[i];
         if (v) atomicAdd(&gh[i], v);
     }
+    DMMT_TRACE(5);
+    DMMT_TRACE_FLUSH(0);
 }
 
 // ============================================================== k_dcdiff
@@ -367,6 +503,7 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
     __shared__ uint32_t sScan[4][256];
     __shared__ int sBits[4][16];
 
+    DMMT_TRACE_START;
     const int tid = threadIdx.x;
     const int tab = tid >> 8;
     const int s = tid & 255;
@@ -392,6 +529,7 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
     if (s < PM_LEVELS) sCnt[tab][s] = 0;
     if (s == 0) sN[tab] = 0;
     __syncthreads();
+    DMMT_TRACE(10);
 
     // ---- 2
     // key = (frequency, symbol), absent symbols last: rank = keys below mine
@@ -418,6 +556,7 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
     }
     if (s == 0 && (n == 0 || ((tab & 1) && sFreq[tab][0xFF] > 0))) atomicOr(status, 2);
     __syncthreads();
+    DMMT_TRACE(11);
 
     // ---- 3
     int size_prev = n;
@@ -454,6 +593,7 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
         size_prev = n + np;
         __syncthreads();
     }
+    DMMT_TRACE(12);
 
     // ---- 4
     int packages = n - 1;
@@ -469,6 +609,7 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
         packages = c - leafs;
     }
     __syncthreads();
+    DMMT_TRACE(13);
     int len = 0;
     if (s < n) {
         for (int k = 0; k < PM_LEVELS; ++k) len += s < sLeaf[tab][k] ? 1 : 0;
@@ -501,6 +642,7 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
         ct[s] = 0;
     }
     __syncthreads();
+    DMMT_TRACE(14);
 
     // ---- 6: header
     uint8_t* o = out + (size_t)frame * out_stride;
@@ -567,6 +709,8 @@ __global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist,
         const int t = tid >> 6, i = tid & 63;
         o[20 + 69 * t + 5 + i] = qtab_u8[t * 64 + c_zigzag[i]];
     }
+    DMMT_TRACE(15);
+    DMMT_TRACE_FLUSH(0);
 }
 
 // ============================================================== operator: DCT only
@@ -689,7 +833,19 @@ static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const
                        hipStream_t st) {
     constexpr int TM = 32 / HR;
     const long long ntiles = (long long)((g.mcux + TM - 1) / TM) * g.mcuy;
-    dim3 grid(clampi(ntiles, 1, (int)(1536 / n_frames > 0 ? 1536 / n_frames : 1)), n_frames);
+    // one workgroup per resident slot: each loops over tiles, prefetching the next
+    static int resident = 0;
+    if (!resident) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_front<HR, VR, S>, 256, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 2;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        resident = per_cu * cus;
+    }
+    dim3 grid(clampi(ntiles, 1, resident / n_frames > 0 ? resident / n_frames : 1), n_frames);
     hipLaunchKernelGGL((k_front<HR, VR, S>), grid, dim3(256), 0, st, (const S*)rgb, stride_elems, g, w.norm_lut,
                        w.qtab, w.coef, w.dc, w.ac_hist, w.status);
 }
@@ -750,3 +906,12 @@ hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_
 }
 
 }  // namespace dmmt
+
+#ifdef DMMT_PHASE_TRACE
+// development builds only: copy out and clear this file's phase counters
+extern "C" int dmmt_debug_trace_kernels(unsigned long long* out64) {
+    if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(dmmt::g_trace), 64 * 8) != hipSuccess) return -1;
+    unsigned long long z[64] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(dmmt::g_trace), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif

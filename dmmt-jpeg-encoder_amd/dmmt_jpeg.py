@@ -25,7 +25,9 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdmmt_jpeg.so")
+# DMMT_LIB_PATH selects another build of the same library (e.g. the
+# `make TRACE=1` development build in lib_trace/)
+LIB_PATH = os.environ.get("DMMT_LIB_PATH") or os.path.join(_HERE, "lib", "libdmmt_jpeg.so")
 CLI_PATH = os.path.join(_HERE, "bin", "dmmt-jpeg-encoder")
 
 try:  # see module docstring: bind the library to torch's HIP runtime if torch is present

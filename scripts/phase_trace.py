@@ -1,0 +1,66 @@
+"""Per-phase cycle counts of the kernels from the `make TRACE=1` build.
+
+Runs the bench workload through lib_trace/libdmmt_jpeg.so and prints, for
+every traced phase, the time per mark (s_memrealtime, 100 MHz) (thread 0 of every
+workgroup marks once per phase pass) and the summed cycles.
+  python scripts/phase_trace.py [--config 4k444q90] [--steps 20]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["DMMT_LIB_PATH"] = os.path.join(ROOT, "dmmt-jpeg-encoder_amd", "lib_trace", "libdmmt_jpeg.so")
+sys.path.insert(0, os.path.join(ROOT, "dmmt-jpeg-encoder_amd"))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+import dmmt_jpeg  # noqa: E402
+import bench  # noqa: E402
+
+NAMES = {
+    "kernels": {0: "front A colour", 1: "front B rows", 2: "front C cols+quant", 3: "front D store",
+                4: "front E symbols", 5: "front hist flush", 10: "tables 1 hist", 11: "tables 2 rank",
+                12: "tables 3 merge", 13: "tables 4 leaves", 14: "tables 5 codes", 15: "tables 6 header"},
+    "entropy": {0: "bits load", 1: "bits walk+sum", 4: "place load+prefix", 5: "place zero",
+                6: "place emit", 7: "place store"},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="4k444q90", choices=sorted(bench.CONFIGS))
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    w, h, sub, q, fps = bench.CONFIGS[args.config]
+    luma, chroma = dmmt_jpeg.quality_tables(q)
+    opt_c = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
+                                                chroma_table=chroma).to_c()
+    enc = dmmt_jpeg.Encoder(0)
+    L = dmmt_jpeg.lib()
+    buf = (ctypes.c_ulonglong * 64)()
+    out_stride = (dmmt_jpeg.max_jpeg_bytes(w, h, sub) + 255) // 256 * 256
+    d_in = enc.malloc(w * h * 3 * fps)
+    d_out = enc.malloc(out_stride * fps)
+    d_len = enc.malloc(4 * fps)
+    enc.fill_synthetic(d_in, w, h, fps)
+    for _ in range(3):
+        enc.encode_device(d_in, fps, w, h, None, d_out, out_stride, d_len, frame_stride=w * h * 3, opt_c=opt_c)
+    enc.synchronize()
+    for tu in ("kernels", "entropy"):
+        getattr(L, f"dmmt_debug_trace_{tu}")(buf)
+    for _ in range(args.steps):
+        enc.encode_device(d_in, fps, w, h, None, d_out, out_stride, d_len, frame_stride=w * h * 3, opt_c=opt_c)
+    enc.synchronize()
+    for tu in ("kernels", "entropy"):
+        getattr(L, f"dmmt_debug_trace_{tu}")(buf)
+        v = list(buf)
+        for i in range(32):
+            if v[32 + i]:
+                print(f"{tu:8s} {i:2d} {NAMES[tu].get(i, '?'):22s} marks/step={v[32 + i] / args.steps:9.1f} "
+                      f"us/mark={v[i] / v[32 + i] / 100:9.3f} us/step(sum over marks)={v[i] / args.steps / 100:12.1f}")
+    enc.close()
+
+
+if __name__ == "__main__":
+    main()
