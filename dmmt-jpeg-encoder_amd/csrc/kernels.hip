@@ -188,6 +188,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
     constexpr int NYB = 32 * VR;     // Y blocks: 32 columns x VR rows
     constexpr int CB = TM;           // chroma blocks per component
     constexpr int BS = 72;           // LDS floats per block: 64 + pad (conflict-free column reads)
+    constexpr int CS = 72;           // int16 block stride of the quantised image (144 B: conflict-free 16-B reads)
     constexpr int NJ = 8 * CB;       // fused jobs (chroma row, chroma block)
     constexpr int SB = (int)sizeof(Sample);
     constexpr int PXB = 8 * HR * 3 * SB;  // raw bytes of one job row
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
                 } else {
                     el = (blk - NYB - CB) * BPM + NLUMA + 1;
                 }
-                int16_t* o = sCoef + el * 64;
+                int16_t* o = sCoef + el * CS;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[zz[i]] = (int16_t)(qv[jj][i >> 1] >> (16 * (i & 1)));
             }
@@ -384,34 +385,45 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
         __syncthreads();
         DMMT_TRACE(2);
 
-        // ---- D: write the tile's blocks (contiguous in emission order) and DCs
+        // ---- D + E, side by side: waves 2-3 store the tile's blocks (contiguous in
+        // emission order) and DCs; in waves 0-1 one thread per block walks its 63 AC
+        // coefficients from registers and counts the run/size symbols
+        // (categorize.rs:132-151): ZRL per 16 zeros before a non-zero, EOB after
+        // trailing zeros.
         const int nmcu_valid = min(TM, g.mcux - mx0);
         const int nblk = nmcu_valid * BPM;
         const long long e0 = (long long)frame * g.bpf + ((long long)my * g.mcux + mx0) * BPM;
-        {
-            const uint4* src = reinterpret_cast<const uint4*>(sCoef);
+        static_assert(NB <= 128, "one symbol-walk thread per block in waves 0-1");
+        if (tid >= 128) {
             uint4* dst = reinterpret_cast<uint4*>(coef + e0 * 64);
-            for (int i = tid; i < nblk * 8; i += 256) dst[i] = src[i];
-            for (int b = tid; b < nblk; b += 256) dc[e0 + b] = sCoef[b * 64];
-        }
-        DMMT_TRACE(3);
-
-        // ---- E: AC run/size symbols (categorize.rs:132-151)
-        {
-            const int wave = tid >> 6, lane = lane_id();
-            for (int b = wave; b < nblk; b += 4) {
-                const int c = sCoef[b * 64 + lane];
-                const unsigned long long nz = __ballot(c != 0) & ~1ull;
-                const int t = (b % BPM) < NLUMA ? 0 : 1;
-                if (lane > 0 && c != 0) {
-                    const unsigned long long below = nz & ((1ull << lane) - 1ull);
-                    const int p = below ? 63 - __clzll(below) : 0;
-                    const int run = lane - p - 1;
-                    atomicAdd(&sHist[t * 256 + (((run & 15) << 4) | category_of(c))], 1u);
-                    if (run >= 16) atomicAdd(&sHist[t * 256 + 0xF0], (uint32_t)(run >> 4));
-                }
-                if (lane == 63 && c == 0) atomicAdd(&sHist[t * 256], 1u);  // EOB
+            for (int i = tid - 128; i < nblk * 8; i += 128)
+                dst[i] = *reinterpret_cast<const uint4*>(sCoef + (i >> 3) * CS + (i & 7) * 8);
+            for (int b = tid - 128; b < nblk; b += 128) dc[e0 + b] = sCoef[b * CS];
+        } else if (tid < nblk) {
+            uint32_t w[32];
+            const uint4* src = reinterpret_cast<const uint4*>(sCoef + tid * CS);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint4 u = src[i];
+                w[4 * i] = u.x;
+                w[4 * i + 1] = u.y;
+                w[4 * i + 2] = u.z;
+                w[4 * i + 3] = u.w;
             }
+            uint32_t* h = sHist + ((tid % BPM) < NLUMA ? 0 : 256);
+            int run = 0;
+#pragma unroll
+            for (int k = 1; k < 64; ++k) {
+                const int v = (k & 1) ? ((int)w[k >> 1] >> 16) : (int)(int16_t)(w[k >> 1] & 0xFFFFu);
+                if (v != 0) {
+                    if (run >= 16) atomicAdd(&h[0xF0], (uint32_t)(run >> 4));
+                    atomicAdd(&h[((run & 15) << 4) | category_of(v)], 1u);
+                    run = 0;
+                } else {
+                    ++run;
+                }
+            }
+            if (run) atomicAdd(&h[0], 1u);  // EOB
         }
         __syncthreads();
         DMMT_TRACE(4);
