@@ -7,31 +7,37 @@
 namespace dmmt {
 
 // Phase tracer for development builds (make TRACE=1): thread 0 of each
-// workgroup accumulates, in registers, the 100-MHz real-time ticks between
-// consecutive marks per phase slot (< 16) and adds them to the translation
-// unit's g_trace (slot 32+i counts the marks) once, at DMMT_TRACE_FLUSH.
-// Compiled out of the product library.
+// workgroup accumulates, in registers, the 100-MHz real-time ticks and the
+// shader-clock cycles between consecutive marks per phase slot (< 16) and adds
+// them to the translation unit's g_trace (slots i, 16+i; 32+i counts the marks)
+// once, at DMMT_TRACE_FLUSH.  Compiled out of the product library.
 #ifdef DMMT_PHASE_TRACE
 #define DMMT_TRACE_START                                                  \
     unsigned long long _dmmt_tr = __builtin_amdgcn_s_memrealtime();       \
-    unsigned long long _dmmt_acc[16];                                     \
+    unsigned long long _dmmt_tc = __builtin_amdgcn_s_memtime();           \
+    unsigned long long _dmmt_acc[16], _dmmt_clk[16];                      \
     unsigned _dmmt_cnt[16];                                               \
     _Pragma("unroll") for (int _i = 0; _i < 16; ++_i) {                   \
         _dmmt_acc[_i] = 0;                                                \
+        _dmmt_clk[_i] = 0;                                                \
         _dmmt_cnt[_i] = 0;                                                \
     }
 #define DMMT_TRACE(i)                                                     \
     do {                                                                  \
         const unsigned long long _n = __builtin_amdgcn_s_memrealtime();   \
+        const unsigned long long _c = __builtin_amdgcn_s_memtime();       \
         _dmmt_acc[(i) & 15] += _n - _dmmt_tr;                             \
+        _dmmt_clk[(i) & 15] += _c - _dmmt_tc;                             \
         _dmmt_cnt[(i) & 15] += 1;                                         \
         _dmmt_tr = _n;                                                    \
+        _dmmt_tc = _c;                                                    \
     } while (0)
 #define DMMT_TRACE_FLUSH(base)                                            \
     do {                                                                  \
         if (threadIdx.x == 0) {                                           \
             _Pragma("unroll") for (int _i = 0; _i < 16; ++_i) if (_dmmt_cnt[_i]) { \
                 atomicAdd(&g_trace[(base) + _i], _dmmt_acc[_i]);          \
+                atomicAdd(&g_trace[16 + (base) + _i], _dmmt_clk[_i]);     \
                 atomicAdd(&g_trace[32 + (base) + _i], (unsigned long long)_dmmt_cnt[_i]); \
             }                                                             \
         }                                                                 \

@@ -148,7 +148,8 @@ struct EmitSink {
 __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, const int16_t* __restrict__ dcdiff,
                                               const uint32_t* __restrict__ code_tab, Geom g,
                                               uint16_t* __restrict__ block_bits, uint32_t* __restrict__ chunk_bits,
-                                              unsigned long long* __restrict__ super_bits) {
+                                              unsigned long long* __restrict__ super_bits,
+                                              uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist) {
     __shared__ uint32_t sTab[4 * 256];
     __shared__ uint32_t sWave[4];
     DMMT_TRACE_START;
@@ -159,6 +160,10 @@ __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, 
     const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
     const long long e = (long long)frame * g.bpf + el0 + tid;
     for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
+    if (chunk == 0) {  // the histogram replicas k_tables read: zero for the next launch
+        for (int i = tid; i < kHistReps * 512; i += 256) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
+        for (int i = tid; i < kHistReps * 32; i += 256) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
+    }
     const bool valid = tid < nb;
     BlockCoef b;
     int dcd = 0;
@@ -417,7 +422,7 @@ __global__ __launch_bounds__(256) void k_stuffwrite(uint32_t* __restrict__ packe
 hipError_t launch_bits(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
     hipLaunchKernelGGL(k_bits, dim3(g.nch, n_frames), dim3(256), 0, st, (const int16_t*)w.coef,
                        (const int16_t*)w.dcdiff, (const uint32_t*)w.code_tab, g, w.block_bits, w.chunk_bits,
-                       w.super_bits);
+                       w.super_bits, w.ac_hist, w.dc_hist);
     return hipGetLastError();
 }
 

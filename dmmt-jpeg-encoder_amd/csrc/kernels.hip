@@ -477,17 +477,26 @@ __global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, 
 }
 
 // ============================================================== k_tables
-// One 1024-thread workgroup per frame; thread group tab = tid/256 builds table
-// tab (0 luma DC, 1 luma AC, 2 chroma DC, 3 chroma AC), thread s = symbol.
-//  1 sum the histogram replicas (and zero them for the next launch)
-//  2 rank symbols by (frequency, symbol): the stable ascending sort of
-//    symbol_counting.rs:92-94 over the f>0 filter of 25-32
-//  3 package-merge, limit 15 (length_limited.rs:37-134): level k = merge of
-//    the pairwise packages of level k-1 with the leaves, ties leaf-first
-//  4 solution from the deepest level (n-1 packages), lengths, +1 on the least
+// One 512-thread workgroup per (table, frame): blockIdx.x = table (0 luma DC,
+// 1 luma AC, 2 chroma DC, 3 chroma AC); thread s < 256 = symbol / leaf s,
+// thread 256 + j = package j.
+//  1 histograms summed over the replicas (k_bits zeroes them after this launch);
+//    every workgroup counts the present symbols of all four tables, which place
+//    the DHT segments
+//  2 compact the present symbols and rank them by (frequency, symbol): the stable
+//    ascending sort of symbol_counting.rs:92-94 over the f>0 filter of 25-32
+//  3 package-merge, limit 15 (length_limited.rs:37-134): level k = merge of the
+//    pairwise packages of level k-1 with the leaves, ties leaf-first.  A leaf's
+//    count of lighter packages never falls from one level to the next and a
+//    package's count of leaves not heavier never rises (every level's items are
+//    no heavier than the previous level's at the same index), so each search
+//    gallops from its previous answer: usually one or two LDS reads per level
+//  4 solution from the deepest level (n-1 packages): a scalar chain over
+//    per-level package bitmasks with word prefix counts; lengths, +1 on the least
 //    frequent symbol (symbol_counting.rs:85-90)
 //  5 canonical codes over the reversed list (huffman/encoder.rs:45-67,116-119)
-//  6 header bytes SOI .. SOS (encoder.rs:125-262)
+//  6 this table's DHT segment; table 0's workgroup also writes SOI, APP0, DQT,
+//    SOF0, [DRI], SOS (encoder.rs:125-262)
 
 #define PM_LEVELS 15
 
@@ -496,230 +505,291 @@ __device__ __forceinline__ void put_be16(uint8_t* p, int v) {
     p[1] = (uint8_t)v;
 }
 
-__global__ __launch_bounds__(1024) void k_tables(uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist,
-                                                 uint32_t* __restrict__ code_tab,  // [frames][4][256]
-                                                 uint8_t* __restrict__ out, size_t out_stride,
-                                                 uint32_t* __restrict__ hdr_len, Geom g,
-                                                 const uint8_t* __restrict__ qtab_u8,  // [2][64] natural
-                                                 int bits_per_channel, int* __restrict__ status) {
-    __shared__ unsigned long long sFreq[4][256];
-    __shared__ unsigned long long sKey[4][256];
-    __shared__ unsigned long long sSortF[4][256];
-    __shared__ uint8_t sSortS[4][256];
-    __shared__ unsigned long long sLev[2][4][512];
-    __shared__ uint8_t sKind[4][PM_LEVELS][512];
-    __shared__ int sN[4];
-    __shared__ int sLeaf[4][PM_LEVELS];
-    __shared__ int sCnt[4][PM_LEVELS];
-    __shared__ int sLen[4][256];
-    __shared__ uint32_t sScan[4][256];
-    __shared__ int sBits[4][16];
+// #{j < m : pair sum prev[2j] + prev[2j+1] < x}, known to be >= lb (sums ascending)
+__device__ __forceinline__ int packages_below(const unsigned long long* prev, int m, unsigned long long x, int lb) {
+    const ulonglong2* pr = reinterpret_cast<const ulonglong2*>(prev);
+    int lo = lb, hi = m, step = 1;  // every j < lo is below x; the answer is in [lo, hi]
+    while (lo < hi) {               // gallop up
+        const int probe = min(lo + step - 1, hi - 1);
+        const ulonglong2 p = pr[probe];
+        if (p.x + p.y < x) {
+            lo = probe + 1;
+            step <<= 1;
+        } else {
+            hi = probe;
+            break;
+        }
+    }
+    while (lo < hi) {  // bisect [lo, hi]
+        const int mid = (lo + hi) >> 1;
+        const ulonglong2 p = pr[mid];
+        if (p.x + p.y < x)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// #{i < m : f[i] <= x}, known to be <= ub (f ascending)
+__device__ __forceinline__ int leaves_not_above(const unsigned long long* f, int m, unsigned long long x, int ub) {
+    int lo = 0, hi = min(ub, m), step = 1;  // every i < lo is <= x, every i >= hi is > x
+    while (lo < hi) {                       // gallop down
+        const int probe = max(hi - step, lo);
+        if (f[probe] <= x) {
+            lo = probe + 1;
+            break;
+        }
+        hi = probe;
+        step <<= 1;
+    }
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (f[mid] <= x)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_hist,
+                                                const uint32_t* __restrict__ dc_hist,
+                                                uint32_t* __restrict__ code_tab,  // [frames][4][256]
+                                                uint8_t* __restrict__ out, size_t out_stride,
+                                                uint32_t* __restrict__ hdr_len, Geom g,
+                                                const uint8_t* __restrict__ qtab_u8,  // [2][64] natural
+                                                int bits_per_channel, int* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) unsigned long long sKey[256];  // present symbols, symbol order
+    __shared__ __attribute__((aligned(16))) unsigned long long sF[256];    // frequencies, ascending
+    __shared__ __attribute__((aligned(16))) unsigned long long sLev[2][512];
+    __shared__ unsigned long long sPk[PM_LEVELS][8];  // package positions per level (bitmask)
+    __shared__ int sPkCum[PM_LEVELS][8];              // packages in the words before
+    __shared__ uint8_t sSym[256];  // symbols by rank
+    __shared__ int sLen[256];      // code length by rank
+    __shared__ int sCnt[4][4];     // [wave][table] present symbols
+    __shared__ int sLeaf[PM_LEVELS];
+    __shared__ uint32_t sWave[4];
+    __shared__ int sBits[16];
 
     DMMT_TRACE_START;
-    const int tid = threadIdx.x;
-    const int tab = tid >> 8;
-    const int s = tid & 255;
-    const int frame = blockIdx.x;
+    const int tab = blockIdx.x, frame = blockIdx.y;
+    const int t = threadIdx.x, lane = lane_id();
+    const int s = t & 255, wave = s >> 6;
+    const bool sym_thread = t < 256;
 
     // ---- 1
-    unsigned long long f = 0;
-    if ((tab & 1) || s < 16) {
-        // all replica loads first (independent, in flight together), then the zeroing stores
-        uint32_t* p0 = (tab & 1) ? &ac_hist[(((size_t)frame * kHistReps) * 2 + (tab >> 1)) * 256 + s]
-                                 : &dc_hist[((size_t)frame * kHistReps) * 32 + (tab >> 1) * 16 + s];
-        const size_t rstride = (tab & 1) ? 512 : 32;
-        uint32_t v[kHistReps];
+    unsigned long long fr[4] = {0, 0, 0, 0};
+    if (sym_thread) {
+        uint32_t va[2][kHistReps], vd[2][kHistReps];
 #pragma unroll
-        for (int r = 0; r < kHistReps; ++r) v[r] = __builtin_nontemporal_load(p0 + r * rstride);
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int r = 0; r < kHistReps; ++r) f += v[r];
+            for (int r = 0; r < kHistReps; ++r) {
+                va[c][r] = ac_hist[(((size_t)frame * kHistReps + r) * 2 + c) * 256 + s];
+                vd[c][r] = s < 16 ? dc_hist[((size_t)frame * kHistReps + r) * 32 + c * 16 + s] : 0u;
+            }
 #pragma unroll
-        for (int r = 0; r < kHistReps; ++r) p0[r * rstride] = 0u;
+        for (int c = 0; c < 2; ++c) {
+            unsigned long long a = 0, d = 0;
+#pragma unroll
+            for (int r = 0; r < kHistReps; ++r) {
+                a += va[c][r];
+                d += vd[c][r];
+            }
+            fr[2 * c] = d;
+            fr[2 * c + 1] = a;
+        }
     }
-    sFreq[tab][s] = f;
-    if (s < 16) sBits[tab][s] = 0;
-    if (s < PM_LEVELS) sCnt[tab][s] = 0;
-    if (s == 0) sN[tab] = 0;
+    const unsigned long long f = fr[tab];
+    const unsigned long long own = __ballot(f > 0);
+    if (sym_thread) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned long long b = __ballot(fr[q] > 0);
+            if (lane == 0) sCnt[wave][q] = __popcll(b);
+        }
+        if (s < 16) sBits[s] = 0;
+    } else if (s < PM_LEVELS * 8) {
+        sPk[s >> 3][s & 7] = 0ull;
+    }
+    __syncthreads();
+    int nt[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) nt[q] = sCnt[0][q] + sCnt[1][q] + sCnt[2][q] + sCnt[3][q];
+    const int n = nt[tab];
+    if (sym_thread && f > 0) {
+        int idx = __popcll(own & ((1ull << lane) - 1ull));
+        for (int w = 0; w < wave; ++w) idx += sCnt[w][tab];
+        sKey[idx] = (f << 8) | (unsigned)s;
+    }
+    if (sym_thread && ((s == 0 && n == 0) || ((tab & 1) && s == 0xFF && f > 0))) atomicOr(status, 2);
     __syncthreads();
     DMMT_TRACE(10);
 
-    // ---- 2
-    // key = (frequency, symbol), absent symbols last: rank = keys below mine
-    int rank = -1;
-    {
-        const unsigned long long mykey = f ? ((f << 8) | (unsigned)s) : ~0ull;
-        sKey[tab][s] = mykey;
-        __syncthreads();
-        if (f > 0) {
-            int r = 0;
-#pragma unroll 16
-            for (int t = 0; t < 256; ++t) r += sKey[tab][t] < mykey ? 1 : 0;
-            rank = r;
-            atomicAdd(&sN[tab], 1);
+    // ---- 2: rank = present keys below mine
+    if (sym_thread && f > 0) {
+        const unsigned long long mykey = (f << 8) | (unsigned)s;
+        const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(sKey);
+        int r = 0;
+        for (int j = 0; j < (n >> 1); ++j) {
+            const ulonglong2 kk = k2[j];
+            r += (kk.x < mykey ? 1 : 0) + (kk.y < mykey ? 1 : 0);
         }
+        if (n & 1) r += sKey[n - 1] < mykey ? 1 : 0;
+        sF[r] = f;
+        sSym[r] = (uint8_t)s;
+        sLev[0][r] = f;
     }
-    __syncthreads();
-    const int n = sN[tab];
-    if (rank >= 0) {
-        sSortF[tab][rank] = f;
-        sSortS[tab][rank] = (uint8_t)s;
-        sLev[0][tab][rank] = f;
-        sKind[tab][0][rank] = 0;
-    }
-    if (s == 0 && (n == 0 || ((tab & 1) && sFreq[tab][0xFF] > 0))) atomicOr(status, 2);
     __syncthreads();
     DMMT_TRACE(11);
 
     // ---- 3
-    int size_prev = n;
-    for (int k = 1; k < PM_LEVELS; ++k) {
-        const unsigned long long* prev = sLev[(k - 1) & 1][tab];
-        unsigned long long* cur = sLev[k & 1][tab];
-        const int np = size_prev >> 1;
-        if (s < n) {  // leaf s: after every package strictly lighter
-            const unsigned long long fl = sSortF[tab][s];
-            int lo = 0, hi = np;  // first package j with P_j >= fl
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (prev[2 * mid] + prev[2 * mid + 1] < fl)
-                    lo = mid + 1;
-                else
-                    hi = mid;
+    {
+        int size_prev = n, np_prev = 0;
+        int cnt = sym_thread ? 0 : n;  // previous answer: lower bound (leaf) / upper bound (package)
+        const unsigned long long fl = sym_thread && s < n ? sF[s] : 0ull;
+        for (int k = 1; k < PM_LEVELS; ++k) {
+            const unsigned long long* prev = sLev[(k - 1) & 1];
+            unsigned long long* cur = sLev[k & 1];
+            const int np = size_prev >> 1;
+            if (sym_thread) {
+                if (s < n) {  // leaf s: after every package strictly lighter
+                    cnt = packages_below(prev, np, fl, cnt);
+                    cur[s + cnt] = fl;
+                }
+            } else if (s < np) {  // package s: after every leaf not heavier
+                const ulonglong2 pp = reinterpret_cast<const ulonglong2*>(prev)[s];
+                const unsigned long long P = pp.x + pp.y;
+                cnt = leaves_not_above(sF, n, P, s < np_prev ? cnt : n);
+                const int pos = s + cnt;
+                cur[pos] = P;
+                atomicOr(&sPk[k][pos >> 6], 1ull << (pos & 63));
             }
-            cur[s + lo] = fl;
-            sKind[tab][k][s + lo] = 0;
+            np_prev = np;
+            size_prev = n + np;
+            __syncthreads();
         }
-        if (s < np) {  // package s: after every leaf not heavier
-            const unsigned long long P = prev[2 * s] + prev[2 * s + 1];
-            int lo = 0, hi = n;  // first leaf with f > P
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (sSortF[tab][mid] <= P)
-                    lo = mid + 1;
-                else
-                    hi = mid;
-            }
-            cur[s + lo] = P;
-            sKind[tab][k][s + lo] = 1;
-        }
-        size_prev = n + np;
-        __syncthreads();
     }
     DMMT_TRACE(12);
 
-    // ---- 4
-    int packages = n - 1;
-    for (int k = PM_LEVELS - 1; k >= 0; --k) {
-        const int c = 2 * packages;
-        const bool l0 = s < c && sKind[tab][k][s] == 0;
-        const bool l1 = s + 256 < c && sKind[tab][k][s + 256] == 0;
-        const unsigned long long b0 = __ballot(l0), b1 = __ballot(l1);
-        if ((tid & 63) == 0) atomicAdd(&sCnt[tab][k], __popcll(b0) + __popcll(b1));
-        __syncthreads();
-        const int leafs = sCnt[tab][k];
-        sLeaf[tab][k] = leafs;  // same value from every thread of the table
-        packages = c - leafs;
+    // ---- 4: leaves in the solution prefix of every level, deepest first: the
+    // prefix of level k holds 2 * (packages taken at level k+1) items; the packages
+    // among them are the ones taken at level k-1
+    if (!sym_thread && s < PM_LEVELS * 8) {
+        const int k = s >> 3, w = s & 7;
+        int c = 0;
+        for (int q = 0; q < w; ++q) c += __popcll(sPk[k][q]);
+        sPkCum[k][w] = c;
+    }
+    __syncthreads();
+    if (t == 0) {
+        int packages = n - 1;
+        for (int k = PM_LEVELS - 1; k >= 0; --k) {
+            const int c = max(2 * packages, 0);  // <= 2n - 2 < 512
+            const int w = c >> 6, b = c & 63;
+            const int pk = sPkCum[k][w] + __popcll(sPk[k][w] & ((1ull << b) - 1ull));
+            sLeaf[k] = c - pk;
+            packages = pk;
+        }
+    }
+    __syncthreads();
+    if (sym_thread && s < n) {
+        int len = s == 0 ? 1 : 0;
+#pragma unroll
+        for (int k = 0; k < PM_LEVELS; ++k) len += s < sLeaf[k] ? 1 : 0;
+        sLen[s] = len;
+        atomicAdd(&sBits[len - 1], 1);
     }
     __syncthreads();
     DMMT_TRACE(13);
-    int len = 0;
-    if (s < n) {
-        for (int k = 0; k < PM_LEVELS; ++k) len += s < sLeaf[tab][k] ? 1 : 0;
-        if (s == 0) len += 1;
-        sLen[tab][s] = len;
-        atomicAdd(&sBits[tab][len - 1], 1);
-    }
-    // ---- 5: code(i) = sum_{t>i} 2^(16 - len_t), exclusive over the reversed list
-    __syncthreads();  // sLen complete
+
+    // ---- 5: code(p) = sum over reversed positions before p of 2^(16 - len)
+    uint32_t* ct = code_tab + ((size_t)frame * 4 + tab) * 256;
     {
-        uint32_t w = 0;
-        if (s < n) w = 1u << (16 - sLen[tab][n - 1 - s]);  // weight at reversed position s
-        sScan[tab][s] = w;
+        const int rk = n - 1 - s;  // rank at reversed position s
+        const uint32_t wgt = sym_thread && s < n ? 1u << (16 - sLen[rk]) : 0u;
+        const uint32_t incl = wave_incl_scan_u32(wgt);
+        if (sym_thread && lane == 63) sWave[wave] = incl;
         __syncthreads();
-        for (int d = 1; d < 256; d <<= 1) {
-            const uint32_t add = s >= d ? sScan[tab][s - d] : 0u;
-            __syncthreads();
-            sScan[tab][s] += add;
-            __syncthreads();
+        uint32_t excl = incl - wgt;
+        for (int q = 0; q < wave; ++q) excl += sWave[q];
+        if (sym_thread && f == 0) ct[s] = 0;
+        __syncthreads();  // the zeroes before the codes (a present symbol's entry is written by another thread)
+        if (sym_thread && s < n) {
+            const int L = sLen[rk];
+            const uint32_t pat = excl & 0xFFFFu;  // left aligned u16 (wrapping as in the reference)
+            ct[sSym[rk]] = ((uint32_t)L << 16) | (pat >> (16 - L));
         }
     }
-    uint32_t* ct = code_tab + ((size_t)frame * 4 + tab) * 256;
-    if (rank >= 0) {
-        const int rpos = n - 1 - rank;  // position in the reversed (most frequent first) list
-        const uint32_t excl = rpos > 0 ? sScan[tab][rpos - 1] : 0u;
-        const int L = sLen[tab][rank];
-        const uint32_t pat = excl & 0xFFFFu;  // left aligned u16 (wrapping as in the reference)
-        ct[s] = ((uint32_t)L << 16) | (pat >> (16 - L));
-    } else {
-        ct[s] = 0;
-    }
-    __syncthreads();
     DMMT_TRACE(14);
 
     // ---- 6: header
+    if (!sym_thread) return;
     uint8_t* o = out + (size_t)frame * out_stride;
-    const int nLAC = sN[1], nLDC = sN[0], nCAC = sN[3], nCDC = sN[2];
     const int pos_dht0 = 2 + 18 + 69 + 69 + 19;
-    const int dht_off[4] = {pos_dht0 + (4 + 17 + nLAC),                                       // luma DC
-                            pos_dht0,                                                         // luma AC
-                            pos_dht0 + (4 + 17 + nLAC) + (4 + 17 + nLDC) + (4 + 17 + nCAC),   // chroma DC
-                            pos_dht0 + (4 + 17 + nLAC) + (4 + 17 + nLDC)};                    // chroma AC
-    const int pos_after_dht = pos_dht0 + 4 * (4 + 17) + nLAC + nLDC + nCAC + nCDC;
-    const int pos_sos = pos_after_dht + (g.restart_interval > 0 ? 6 : 0);
-    // DHT symbols in reversed order (encoder.rs:180)
-    if (rank >= 0) o[dht_off[tab] + 4 + 17 + (n - 1 - rank)] = (uint8_t)s;
-    if (s < 16) o[dht_off[tab] + 5 + s] = (uint8_t)sBits[tab][s];
+    const int off_lac = pos_dht0;
+    const int off_ldc = off_lac + 21 + nt[1];
+    const int off_cac = off_ldc + 21 + nt[0];
+    const int off_cdc = off_cac + 21 + nt[3];
+    const int dht = tab == 0 ? off_ldc : tab == 1 ? off_lac : tab == 2 ? off_cdc : off_cac;
+    if (s < n) o[dht + 21 + s] = sSym[n - 1 - s];  // DHT symbols in reversed order (encoder.rs:180)
+    if (s < 16) o[dht + 5 + s] = (uint8_t)sBits[s];
     if (s == 0) {
-        uint8_t* d = o + dht_off[tab];
+        uint8_t* d = o + dht;
         d[0] = 0xFF;
         d[1] = 0xC4;
         put_be16(d + 2, 2 + 17 + n);
         const uint8_t kind[4] = {0x00, 0x11, 0x02, 0x13};  // encoder.rs:92-98 TableKind
         d[4] = kind[tab];
     }
-    if (tid == 0) {
-        o[0] = 0xFF;
-        o[1] = 0xD8;  // SOI
-        const uint8_t app0[18] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0, 0x01, 0x02, 0x00, 0x00, 0x48, 0x00, 0x48, 0, 0};
-        for (int i = 0; i < 18; ++i) o[2 + i] = app0[i];
-        for (int t = 0; t < 2; ++t) {  // DQT, table in zigzag order (encoder.rs:193-212)
-            uint8_t* d = o + 20 + 69 * t;
-            d[0] = 0xFF;
-            d[1] = 0xDB;
-            put_be16(d + 2, 67);
-            d[4] = (uint8_t)t;
+    if (tab == 0) {
+        const int pos_after_dht = pos_dht0 + 4 * 21 + nt[0] + nt[1] + nt[2] + nt[3];
+        const int pos_sos = pos_after_dht + (g.restart_interval > 0 ? 6 : 0);
+        if (s == 0) {
+            o[0] = 0xFF;
+            o[1] = 0xD8;  // SOI
+            const uint8_t app0[18] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0, 0x01, 0x02, 0x00, 0x00, 0x48, 0x00, 0x48, 0, 0};
+            for (int i = 0; i < 18; ++i) o[2 + i] = app0[i];
+            for (int q = 0; q < 2; ++q) {  // DQT, table in zigzag order (encoder.rs:193-212)
+                uint8_t* d = o + 20 + 69 * q;
+                d[0] = 0xFF;
+                d[1] = 0xDB;
+                put_be16(d + 2, 67);
+                d[4] = (uint8_t)q;
+            }
+            uint8_t* sof = o + 158;  // encoder.rs:227-245
+            sof[0] = 0xFF;
+            sof[1] = 0xC0;
+            put_be16(sof + 2, 17);
+            sof[4] = (uint8_t)bits_per_channel;
+            put_be16(sof + 5, g.height);
+            put_be16(sof + 7, g.width);
+            sof[9] = 3;
+            sof[10] = 1;
+            sof[11] = (uint8_t)((g.hr << 4) | g.vr);
+            sof[12] = 0;
+            sof[13] = 2;
+            sof[14] = 0x11;
+            sof[15] = 1;
+            sof[16] = 3;
+            sof[17] = 0x11;
+            sof[18] = 1;
+            if (g.restart_interval > 0) {  // extension: DRI
+                uint8_t* d = o + pos_after_dht;
+                d[0] = 0xFF;
+                d[1] = 0xDD;
+                put_be16(d + 2, 4);
+                put_be16(d + 4, g.restart_interval);
+            }
+            const uint8_t sos[14] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x01, 0x02, 0x23, 0x03, 0x23, 0x00, 0x3F, 0x00};
+            for (int i = 0; i < 14; ++i) o[pos_sos + i] = sos[i];
+            hdr_len[frame] = (uint32_t)(pos_sos + 14);
         }
-        uint8_t* sof = o + 158;  // encoder.rs:227-245
-        sof[0] = 0xFF;
-        sof[1] = 0xC0;
-        put_be16(sof + 2, 17);
-        sof[4] = (uint8_t)bits_per_channel;
-        put_be16(sof + 5, g.height);
-        put_be16(sof + 7, g.width);
-        sof[9] = 3;
-        sof[10] = 1;
-        sof[11] = (uint8_t)((g.hr << 4) | g.vr);
-        sof[12] = 0;
-        sof[13] = 2;
-        sof[14] = 0x11;
-        sof[15] = 1;
-        sof[16] = 3;
-        sof[17] = 0x11;
-        sof[18] = 1;
-        if (g.restart_interval > 0) {  // extension: DRI
-            uint8_t* d = o + pos_after_dht;
-            d[0] = 0xFF;
-            d[1] = 0xDD;
-            put_be16(d + 2, 4);
-            put_be16(d + 4, g.restart_interval);
+        if (s < 128) {
+            const int q = s >> 6, i = s & 63;
+            o[20 + 69 * q + 5 + i] = qtab_u8[q * 64 + c_zigzag[i]];
         }
-        const uint8_t sos[14] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x01, 0x02, 0x23, 0x03, 0x23, 0x00, 0x3F, 0x00};
-        for (int i = 0; i < 14; ++i) o[pos_sos + i] = sos[i];
-        hdr_len[frame] = (uint32_t)(pos_sos + 14);
-    }
-    if (tid < 128) {
-        const int t = tid >> 6, i = tid & 63;
-        o[20 + 69 * t + 5 + i] = qtab_u8[t * 64 + c_zigzag[i]];
     }
     DMMT_TRACE(15);
     DMMT_TRACE_FLUSH(0);
@@ -899,7 +969,8 @@ hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t
 
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st) {
-    hipLaunchKernelGGL(k_tables, dim3(n_frames), dim3(1024), 0, st, w.ac_hist, w.dc_hist, w.code_tab, out, out_stride,
+    hipLaunchKernelGGL(k_tables, dim3(4, n_frames), dim3(512), 0, st, (const uint32_t*)w.ac_hist,
+                       (const uint32_t*)w.dc_hist, w.code_tab, out, out_stride,
                        w.hdr_len, g, w.qtab_u8, bits_per_channel, w.status);
     return hipGetLastError();
 }

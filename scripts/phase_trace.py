@@ -20,7 +20,7 @@ import bench  # noqa: E402
 
 NAMES = {
     "kernels": {0: "front A colour", 1: "front B rows", 2: "front C cols+quant", 3: "front D store",
-                4: "front E symbols", 5: "front hist flush", 10: "tables 1 hist", 11: "tables 2 rank",
+                4: "front E symbols", 5: "front hist flush", 10: "tables 1 hist", 6: "tables merge leafsearch", 7: "tables merge pkgsearch", 8: "tables merge barrier", 11: "tables 2 rank",
                 12: "tables 3 merge", 13: "tables 4 leaves", 14: "tables 5 codes", 15: "tables 6 header"},
     "entropy": {0: "bits load", 1: "bits walk+sum", 4: "place load+prefix", 5: "place zero",
                 6: "place emit", 7: "place store"},
@@ -55,10 +55,11 @@ def main():
     for tu in ("kernels", "entropy"):
         getattr(L, f"dmmt_debug_trace_{tu}")(buf)
         v = list(buf)
-        for i in range(32):
+        for i in range(16):
             if v[32 + i]:
                 print(f"{tu:8s} {i:2d} {NAMES[tu].get(i, '?'):22s} marks/step={v[32 + i] / args.steps:9.1f} "
-                      f"us/mark={v[i] / v[32 + i] / 100:9.3f} us/step(sum over marks)={v[i] / args.steps / 100:12.1f}")
+                      f"us/mark={v[i] / v[32 + i] / 100:9.3f} us/step(sum over marks)={v[i] / args.steps / 100:12.1f} "
+                      f"clock={v[16 + i] / max(v[i], 1) * 100:6.0f} MHz")
     enc.close()
 
 
