@@ -21,7 +21,7 @@ using namespace dmmt;
 
 namespace {
 
-const char* kStageNames[ST_COUNT] = {"front", "dcdiff", "tables", "bits", "place", "ffcount", "stuffwrite", "ac_hist"};
+const char* kStageNames[ST_COUNT] = {"front", "dcdiff", "tables", "emit", "offsets", "stuffwrite", "ac_hist"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -50,8 +50,8 @@ struct dmmt_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grown on demand, never shrunk)
-    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_bits, packed, block_bits, chunk_bits,
-        super_bits, seg_ff, super_ff, status, lut, qtab, qtab_u8;
+    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_bits, total_ff, stage, chunk_bits, chunk_ff,
+        chunk_edge, chunk_bit0, chunk_ffpre, status, lut, qtab, qtab_u8;
     // host-API staging
     DevBuf in, out, out_len, dct;
     // uploaded table state
@@ -160,34 +160,38 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     if ((rc = ensure(c->coef, nb * 64 * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dc, nb * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dcdiff, nb * sizeof(int16_t)))) return rc;
-    if ((rc = ensure(c->block_bits, nb * sizeof(uint16_t)))) return rc;
+    // staging slots sized for the worst case; k_stuffwrite reads up to 4 words
+    // past a slot's last bit, hence the tail
+    if ((rc = ensure(c->stage, (nch * (size_t)kChunkWordsCap + 64) * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(c->chunk_bits, nch * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c->super_bits, (size_t)nf * (size_t)g.nsuper * 8))) return rc;
-    if ((rc = ensure(c->seg_ff, (size_t)nf * (size_t)g.nseg_cap * 4))) return rc;
-    if ((rc = ensure(c->super_ff, (size_t)nf * (size_t)g.nsuper_seg * 8))) return rc;
+    if ((rc = ensure(c->chunk_ff, nch * 8 * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c->chunk_edge, nch * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c->chunk_bit0, nch * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(c->chunk_ffpre, nch * sizeof(uint32_t)))) return rc;
+    // k_front / k_dcdiff add into the replicas, k_emit zeroes them after k_tables:
+    // zero between launches, starting with the allocation
     if ((rc = ensure(c->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
     if ((rc = ensure(c->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
     if ((rc = ensure(c->code_tab, (size_t)nf * 1024 * 4))) return rc;
     if ((rc = ensure(c->hdr_len, (size_t)nf * 4))) return rc;
     if ((rc = ensure(c->total_bits, (size_t)nf * 8))) return rc;
-    // k_pack ORs the chunk-edge words into this buffer and k_stuff zeroes what it read:
-    // it is all zero between launches, starting with the allocation
-    if ((rc = ensure(c->packed, (size_t)nf * (size_t)g.packed_words * 4, true))) return rc;
+    if ((rc = ensure(c->total_ff, (size_t)nf * 8))) return rc;
     if ((rc = ensure(c->status, 16, true))) return rc;
     w->coef = (int16_t*)c->coef.p;
     w->dc = (int16_t*)c->dc.p;
     w->dcdiff = (int16_t*)c->dcdiff.p;
-    w->block_bits = (uint16_t*)c->block_bits.p;
-    w->chunk_bits = (uint32_t*)c->chunk_bits.p;
-    w->super_bits = (unsigned long long*)c->super_bits.p;
-    w->seg_ff = (uint32_t*)c->seg_ff.p;
-    w->super_ff = (unsigned long long*)c->super_ff.p;
     w->ac_hist = (uint32_t*)c->ac_hist.p;
     w->dc_hist = (uint32_t*)c->dc_hist.p;
     w->code_tab = (uint32_t*)c->code_tab.p;
     w->hdr_len = (uint32_t*)c->hdr_len.p;
     w->total_bits = (unsigned long long*)c->total_bits.p;
-    w->packed = (uint32_t*)c->packed.p;
+    w->stage = (uint32_t*)c->stage.p;
+    w->chunk_bits = (uint32_t*)c->chunk_bits.p;
+    w->chunk_ff = (uint32_t*)c->chunk_ff.p;
+    w->chunk_edge = (uint32_t*)c->chunk_edge.p;
+    w->chunk_bit0 = (unsigned long long*)c->chunk_bit0.p;
+    w->chunk_ffpre = (uint32_t*)c->chunk_ffpre.p;
+    w->total_ff = (unsigned long long*)c->total_ff.p;
     w->status = (int*)c->status.p;
     w->norm_lut = nullptr;  // bound by prepare() after upload_tables
     w->qtab = nullptr;
@@ -254,8 +258,9 @@ struct StageTimer {
     }
 };
 
-// Enqueue the entropy back half (k_dcdiff, k_tables, k_pack, k_stuff) for
-// coefficients already in w.coef / w.dc with AC histograms accumulated.
+// Enqueue the entropy back half (k_dcdiff, k_tables, k_emit, k_offsets,
+// k_stuffwrite) for coefficients already in w.coef / w.dc with AC histograms
+// accumulated.
 int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bits, uint8_t* out, size_t out_stride,
                       uint32_t* out_len, hipStream_t st) {
     {
@@ -267,16 +272,12 @@ int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bit
         HIP_TRY(launch_tables(nf, g, w, bits, out, out_stride, st));
     }
     {
-        StageTimer t(c, ST_BITS, st);
-        HIP_TRY(launch_bits(nf, g, w, st));
+        StageTimer t(c, ST_EMIT, st);
+        HIP_TRY(launch_emit(nf, g, w, st));
     }
     {
-        StageTimer t(c, ST_PLACE, st);
-        HIP_TRY(launch_place(nf, g, w, st));
-    }
-    {
-        StageTimer t(c, ST_FFCOUNT, st);
-        HIP_TRY(launch_ffcount(nf, g, w, st));
+        StageTimer t(c, ST_OFFSETS, st);
+        HIP_TRY(launch_offsets(nf, g, w, st));
     }
     {
         StageTimer t(c, ST_STUFFWRITE, st);
@@ -356,15 +357,13 @@ int take_status(dmmt_ctx* c, hipStream_t st) {
     int s = 0;
     HIP_TRY(hipMemcpyAsync(&s, c->status.p, sizeof s, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (s) HIP_TRY(hipMemsetAsync(c->status.p, 0, sizeof(int), st));
-    if (s & (4 | 8 | 16)) {  // an aborted pack/stuff may leave packed words behind: restore the all-zero invariant
-        if (c->packed.p) HIP_TRY(hipMemsetAsync(c->packed.p, 0, c->packed.bytes, st));
+    if (s) {
+        HIP_TRY(hipMemsetAsync(c->status.p, 0, sizeof(int), st));
         HIP_TRY(hipStreamSynchronize(st));
     }
     if (s & 1) return DMMT_E_VALUE_EXCEEDS_MAX;
     if (s & 2) return DMMT_E_HUFFMAN_SYMBOL_MISSING;
-    if (s & 4) return DMMT_E_HIP;
-    if (s & (8 | 16)) return DMMT_E_CAPACITY;
+    if (s & 16) return DMMT_E_CAPACITY;
     return DMMT_OK;
 }
 
@@ -409,11 +408,11 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     drain_events(c);
     destroy_graphs(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
-    DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff,     &c->ac_hist,    &c->dc_hist,
-                      &c->code_tab,   &c->hdr_len,    &c->total_bits, &c->packed,     &c->block_bits,
-                      &c->chunk_bits, &c->super_bits, &c->seg_ff,     &c->super_ff,   &c->status,
-                      &c->lut,        &c->qtab,       &c->qtab_u8,    &c->in,         &c->out,
-                      &c->out_len,    &c->dct};
+    DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff,     &c->ac_hist,     &c->dc_hist,
+                      &c->code_tab,   &c->hdr_len,    &c->total_bits, &c->total_ff,    &c->stage,
+                      &c->chunk_bits, &c->chunk_ff,   &c->chunk_edge, &c->chunk_bit0,  &c->chunk_ffpre,
+                      &c->status,     &c->lut,        &c->qtab,       &c->qtab_u8,     &c->in,
+                      &c->out,        &c->out_len,    &c->dct};
     for (DevBuf* b : bufs) release(*b);
     (void)hipStreamDestroy(c->stream);
     delete c;

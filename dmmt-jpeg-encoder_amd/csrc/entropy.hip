@@ -1,27 +1,27 @@
-// entropy.hip -- gfx950 entropy-coding back half: bit packing and byte stuffing.
+// entropy.hip -- gfx950 entropy-coding back half: Huffman bit emission and byte
+// stuffing.  [encoder.rs:264-404 write_image_data / write_{dc,ac}_from_block,
+// binary_stream.rs:38-96 BitWriter, segment_marker_injector.rs:13-30]
 //
-// Four launches, no inter-workgroup waiting anywhere:
-//  k_bits        one workgroup per chunk of kChunkBlocks blocks: bits of every
-//                block (kept for k_place) and the chunk total; the total is also
-//                added into its "super" counter (kSuper chunks per super).
-//  k_place       one workgroup per chunk: its bit offset in the frame's scan is
-//                the sum of the supers before it plus the chunk totals before it
-//                in its own super (a few dozen L2 reads), block offsets by a
-//                wave scan, every code placed MSB-first into an LDS word image
-//                which goes out byte-swapped (memory order = stream order).
-//                [encoder.rs:264-404 write_image_data / write_{dc,ac}_from_block,
-//                binary_stream.rs:38-66 BitWriter]
-//  k_ffcount     0xFF bytes per kStuffSeg-byte segment of the packed scan (+ super
-//                counters), the last byte padded with 1-bits (binary_stream.rs:89-96)
-//  k_stuffwrite  segment offset from the same two-level sums; the bytes after the
-//                header with a 0x00 after every 0xFF (segment_marker_injector.rs:13-30),
-//                EOI (encoder.rs:131), file size; zeroes the packed words it read so
-//                the next launch's k_place can OR into a clean buffer.
-//
-// The bit passes run one thread per block (256 blocks per workgroup): the walk
-// over a block's 64 coefficients is serial by nature and cheapest as a fully
-// unrolled register loop; the workgroup scan of the block bit counts gives
-// every thread its exact bit position.
+// Three launches, no inter-workgroup waiting anywhere:
+//  k_emit        one workgroup per chunk of kChunkBlocks blocks, one thread per
+//                block: the bits of every block (a register walk), a workgroup
+//                scan for the block offsets inside the chunk, every code placed
+//                MSB-first into an LDS word image of the chunk's own bit stream,
+//                which goes to the chunk's staging slot.  Per chunk it also
+//                records its bit count, its first and last 16 bits and, for each
+//                of the 8 residues the chunk's start can have modulo 8, the 0xFF
+//                bytes lying wholly inside it -- so no later pass re-reads the
+//                stream to count them.
+//  k_offsets     one workgroup per frame: scan of the chunk bit counts (every
+//                chunk's bit offset); each chunk's 0xFF count at its actual
+//                alignment plus the byte it shares with the next chunk (built from
+//                the recorded edge bits); scan of those (every chunk's offset in
+//                the stuffed scan).
+//  k_stuffwrite  one workgroup per chunk: the bytes whose first bit lies in the
+//                chunk, shifted out of its staging slot (the last one built from
+//                the edge bits, 1-padded at the end of the scan), a 0x00 after
+//                every 0xFF, staged in LDS and stored coalesced after the header;
+//                EOI and the file size by the frame's last chunk.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -35,20 +35,14 @@ namespace dmmt {
 static __device__ unsigned long long g_trace[64];
 #endif
 
-// Sum of the counters before index `i` of a two-level (super, item) counter set,
-// by one wave: supers [0, i/kSuper) + items [kSuper*(i/kSuper), i).
-template <typename T>
-__device__ __forceinline__ unsigned long long prefix_two_level(const unsigned long long* __restrict__ supers,
-                                                               const T* __restrict__ items, unsigned i) {
-    const int lane = lane_id();
-    const unsigned s = i / kSuper;
-    unsigned long long acc = 0;
-    for (unsigned j = (unsigned)lane; j < s; j += 64) acc += supers[j];
-    for (unsigned j = s * kSuper + (unsigned)lane; j < i; j += 64) acc += (unsigned long long)items[j];
-    return wave_sum_u64(acc);
-}
-
 static_assert(kChunkBlocks == 256, "one thread per block, one workgroup per chunk");
+
+// LDS word window of k_emit: 128 Ki bits = 512 bits per block on average (the 4K
+// q90 workload averages ~110).  A chunk with more is emitted in several windows,
+// every block re-walking its codes and keeping only the words inside the window.
+constexpr int kEmitWords = 4096;
+// Bytes per pass of k_stuffwrite (16 per thread).
+constexpr int kStuffPass = 4096;
 
 // One thread walks one block (64 zigzag coefficients held in 32 registers) in
 // stream order (encoder.rs:356-404; categorize.rs:132-169): DC code + extra bits,
@@ -110,23 +104,24 @@ struct CountSink {
     __device__ __forceinline__ void operator()(uint32_t, int len) { n += (uint32_t)len; }
 };
 
-// Appends pieces MSB-first into a word image: words wholly inside the block are
-// stored plainly, the first and last (shared with the neighbouring blocks) are
-// ORed atomically.  LDS image = MSB-first words; global image (slow path) =
-// byte-swapped words (memory order = stream order).
-struct EmitSink {
+// Appends pieces MSB-first into the LDS window image of words [lo, lo + n): the
+// first and the last word of a block (shared with its neighbours) are ORed, the
+// others stored plainly; words outside the window are dropped.
+struct WindowSink {
     uint32_t* img;
-    bool lds;
+    int lo, n;
     unsigned long long acc;
-    int nacc;     // bits pending in acc
-    size_t w;     // next word index
+    int nacc;  // bits pending in acc (< 32 between pieces)
+    int w;     // word index of the pending bits
     bool first;
     __device__ __forceinline__ void put(uint32_t word, bool shared) {
-        const uint32_t v = lds ? word : __builtin_bswap32(word);
-        if (shared)
-            atomicOr(&img[w], v);
-        else
-            img[w] = v;
+        const int i = w - lo;
+        if ((unsigned)i < (unsigned)n) {
+            if (shared)
+                atomicOr(&img[i], word);
+            else
+                img[i] = word;
+        }
     }
     __device__ __forceinline__ void operator()(uint32_t val, int len) {
         acc = (acc << len) | val;
@@ -144,14 +139,24 @@ struct EmitSink {
     }
 };
 
-// ---------------------------------------------------------------------- k_bits
-__global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, const int16_t* __restrict__ dcdiff,
+// 16 bits of an MSB-first word stream starting at bit p (p & 31 taken; words a, b
+// hold bits from (p & ~31))
+__device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
+    const unsigned long long x = ((unsigned long long)a << 32) | b;
+    return (uint32_t)(x >> (48 - (p & 31))) & 0xFFFFu;
+}
+
+// ---------------------------------------------------------------------- k_emit
+__global__ __launch_bounds__(256) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
                                               const uint32_t* __restrict__ code_tab, Geom g,
-                                              uint16_t* __restrict__ block_bits, uint32_t* __restrict__ chunk_bits,
-                                              unsigned long long* __restrict__ super_bits,
+                                              uint32_t* __restrict__ stage, uint32_t* __restrict__ chunk_bits,
+                                              uint32_t* __restrict__ chunk_ff, uint32_t* __restrict__ chunk_edge,
                                               uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist) {
     __shared__ uint32_t sTab[4 * 256];
+    __shared__ uint32_t sW[kEmitWords + 2];
     __shared__ uint32_t sWave[4];
+    __shared__ uint32_t sFF[8];
+    __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     DMMT_TRACE_START;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
@@ -159,300 +164,318 @@ __global__ __launch_bounds__(256) void k_bits(const int16_t* __restrict__ coef, 
     const long long el0 = (long long)chunk * kChunkBlocks;
     const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
     const long long e = (long long)frame * g.bpf + el0 + tid;
+    const size_t cid = (size_t)frame * g.nch + chunk;
     for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
     if (chunk == 0) {  // the histogram replicas k_tables read: zero for the next launch
         for (int i = tid; i < kHistReps * 512; i += 256) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
         for (int i = tid; i < kHistReps * 32; i += 256) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
     }
+    if (tid < 8) sFF[tid] = 0u;
+    if (tid < 3) sEdge[tid] = 0u;
     const bool valid = tid < nb;
-    BlockCoef b;
     int dcd = 0;
-    if (valid) {
-        load_block(coef + e * 64, b);
-        dcd = dcdiff[e];
-    }
-    __syncthreads();
-    DMMT_TRACE(0);
     uint32_t bits = 0;
-    if (valid) {
-        const int k = ((int)(el0 % g.bpm) + tid) % g.bpm;
-        const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
-        CountSink cs;
-        walk_block(b, dcd, tb, tb + 256, cs);
-        bits = cs.n;
-        block_bits[e] = (uint16_t)bits;
-    }
-    const uint32_t ws = wave_sum_u32(bits);
-    if (lane == 0) sWave[wave] = ws;
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
-        chunk_bits[(size_t)frame * g.nch + chunk] = total;
-        atomicAdd(&super_bits[(size_t)frame * g.nsuper + chunk / kSuper], (unsigned long long)total);
-    }
-    DMMT_TRACE(1);
-    DMMT_TRACE_FLUSH(0);
-}
-
-// --------------------------------------------------------------------- k_place
-// LDS word image capacity of one chunk: 128 Ki bits = 512 bits per block on
-// average (the 4K q90 workload averages ~110).  A chunk that needs more (worst
-// case kMaxBlockBits per block) writes straight into the zeroed global buffer
-// instead: slower, same bytes.
-constexpr int kPackWords = 4096;
-
-__global__ __launch_bounds__(256) void k_place(const int16_t* __restrict__ coef, const int16_t* __restrict__ dcdiff,
-                                               const uint32_t* __restrict__ code_tab, Geom g,
-                                               const uint16_t* __restrict__ block_bits,
-                                               const uint32_t* __restrict__ chunk_bits,
-                                               const unsigned long long* __restrict__ super_bits,
-                                               unsigned long long* __restrict__ total_bits,
-                                               uint32_t* __restrict__ packed, int* __restrict__ status) {
-    __shared__ uint32_t sW[kPackWords + 2];
-    __shared__ uint32_t sTab[4 * 256];
-    __shared__ uint32_t sWave[4];
-    __shared__ unsigned long long sBase;
-    DMMT_TRACE_START;
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.y;
-    const unsigned chunk = blockIdx.x;
-    const long long el0 = (long long)chunk * kChunkBlocks;
-    const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
-    const long long e = (long long)frame * g.bpf + el0 + tid;
-    for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
-    const bool valid = tid < nb;
-    BlockCoef b;
-    int dcd = 0;
-    uint32_t mine = 0;
-    if (valid) {
-        load_block(coef + e * 64, b);
-        dcd = dcdiff[e];
-        mine = block_bits[e];
-    }
-    // block offsets within the chunk: workgroup scan of the block bit counts
-    const uint32_t incl = wave_incl_scan_u32(mine);
-    if (lane == 63) sWave[wave] = incl;
-    if (wave == 0) {
-        const unsigned long long pre =
-            prefix_two_level(super_bits + (size_t)frame * g.nsuper, chunk_bits + (size_t)frame * g.nch, chunk);
-        if (lane == 0) sBase = pre;
-    }
-    __syncthreads();
-    DMMT_TRACE(4);
-    uint32_t wpre = 0;
-    for (int w = 0; w < wave; ++w) wpre += sWave[w];
-    const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
-    const unsigned long long bit0 = sBase;
-    if (tid == 0 && chunk == (unsigned)g.nch - 1) total_bits[frame] = bit0 + total;
-    const int shift = (int)(bit0 & 31);
-    const int nw = (int)((shift + (unsigned long long)total + 31) >> 5);
-    if (((bit0 + total + 31) >> 5) + 1 > (unsigned long long)g.packed_words) {
-        if (tid == 0) atomicOr(status, 8);
-        return;  // uniform; the host reports DMMT_E_CAPACITY
-    }
-    uint32_t* const pk = packed + (size_t)frame * g.packed_words + (bit0 >> 5);
-    const bool in_lds = nw + 1 <= kPackWords + 2;
-    if (in_lds)
-        for (int i = tid; i < nw + 1; i += 256) sW[i] = 0u;
-    __syncthreads();
-    DMMT_TRACE(5);
-    if (valid) {
-        const int k = ((int)(el0 % g.bpm) + tid) % g.bpm;
-        const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
-        const uint32_t start = (uint32_t)shift + wpre + incl - mine;  // bit position in the image
-        EmitSink es{in_lds ? sW : pk, in_lds, 0ull, (int)(start & 31), (size_t)(start >> 5), true};
-        walk_block(b, dcd, tb, tb + 256, es);
-        es.finish();
-    }
-    __syncthreads();
-    DMMT_TRACE(6);
-    if (in_lds) {  // interior words plain, the two edge words ORed (shared with neighbouring chunks)
-        for (int i = tid; i < nw; i += 256) {
-            const uint32_t v = __builtin_bswap32(sW[i]);
-            if (i == 0 || i == nw - 1)
-                atomicOr(&pk[i], v);
-            else
-                pk[i] = v;
+    const int k = valid ? ((int)(el0 % g.bpm) + tid) % g.bpm : 0;
+    const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
+    {
+        BlockCoef b;
+        if (valid) {
+            load_block(coef + e * 64, b);
+            dcd = dcdiff[e];
+        }
+        __syncthreads();
+        DMMT_TRACE(0);
+        // bits of every block; offsets inside the chunk by a workgroup scan
+        if (valid) {
+            CountSink cs;
+            walk_block(b, dcd, tb, tb + 256, cs);
+            bits = cs.n;
         }
     }
-    DMMT_TRACE(7);
-    DMMT_TRACE_FLUSH(0);
-}
+    const uint32_t incl = wave_incl_scan_u32(bits);
+    if (lane == 63) sWave[wave] = incl;
+    __syncthreads();
+    uint32_t start = incl - bits;
+    for (int q = 0; q < wave; ++q) start += sWave[q];
+    const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
+    DMMT_TRACE(1);
 
-// ------------------------------------------------------------------- stuffing
-struct ScanBytes {
-    unsigned long long nbytes;
-    unsigned pad;  // 1-bits padding the last byte
-    unsigned nseg;
-};
-
-__device__ __forceinline__ ScanBytes scan_bytes(unsigned long long tb) {
-    ScanBytes s;
-    s.nbytes = (tb + 7) >> 3;
-    s.pad = (unsigned)((8 - (tb & 7)) & 7);
-    s.nseg = (unsigned)((s.nbytes + kStuffSeg - 1) / kStuffSeg);
-    return s;
-}
-
-// The 16 scan bytes of thread `tid` in segment `seg` (the last byte 1-padded) and
-// their 0xFF count; with `clear` also zeroes the packed words read (k_stuffwrite:
-// restores the all-zero invariant for the next launch's k_place).
-__device__ __forceinline__ uint32_t load16(uint8_t* __restrict__ pb, const ScanBytes& s, unsigned seg, int tid,
-                                           uint8_t (&v)[16], bool clear) {
-    const unsigned long long b0 = (unsigned long long)seg * kStuffSeg + (unsigned)tid * 16u;
-    if (b0 + 16 <= s.nbytes) {
-        const uint4 q = *reinterpret_cast<const uint4*>(pb + b0);
-        const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+    uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
+    const int nw = (int)((total + 31) >> 5);
+    const int we1 = total >= 16 ? (int)((total - 16) >> 5) : 0;  // word holding bit total-16
+    uint32_t ff[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int w0 = 0; w0 < nw; w0 += kEmitWords) {  // uniform; one window unless the chunk is huge
+        const int wn = min(kEmitWords, nw - w0);
+        for (int i = tid; i <= wn; i += 256) sW[i] = 0u;  // + the next window's first word
+        __syncthreads();
+        if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
+            // the block again (L2 / MALL): holding it in registers across the scan
+            // would halve the occupancy of this kernel
+            BlockCoef b;
+            load_block(coef + e * 64, b);
+            WindowSink ws{sW, w0, wn + 1, 0ull, (int)(start & 31), (int)(start >> 5), true};
+            walk_block(b, dcd, tb, tb + 256, ws);
+            ws.finish();
+        }
+        __syncthreads();
+        for (int i = tid; i < wn; i += 256) {
+            const uint32_t a = sW[i], c = sW[i + 1];
+            slot[w0 + i] = a;
+            const int wi = w0 + i;
+            if (wi == 0) sEdge[0] = a;
+            if (wi == we1) {  // the pair holding the last 16 bits (c is zero past the end)
+                sEdge[1] = a;
+                sEdge[2] = c;
+            }
+            // runs of 8 ones starting at bit p of word a: bit 31-p of m
+            const unsigned long long x = ((unsigned long long)a << 32) | c;
+            unsigned long long z = x & (x << 1);
+            z &= z << 2;
+            z &= z << 4;
+            const uint32_t m = (uint32_t)(z >> 32);
+            if (m) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = (uint8_t)(wv[j >> 2] >> (8 * (j & 3)));
-        if (clear) *reinterpret_cast<uint4*>(pb + b0) = make_uint4(0, 0, 0, 0);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = b0 + j < s.nbytes ? pb[b0 + j] : 0;
-        if (clear) {
-            const unsigned long long wend = (s.nbytes + 3) >> 2;
-            for (int j = 0; j < 4; ++j) {
-                const unsigned long long wi = (b0 >> 2) + j;
-                if (wi < wend) reinterpret_cast<uint32_t*>(pb)[wi] = 0u;
+                for (int r = 0; r < 8; ++r) ff[r] += __popc(m & (0x80808080u >> r));
             }
         }
-    }
-    const unsigned long long last = s.nbytes - 1;
-    if (s.pad && b0 <= last && last < b0 + 16) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (b0 + j == last) v[j] |= (uint8_t)((1u << s.pad) - 1u);
-    }
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) cnt += (b0 + j < s.nbytes && v[j] == 0xFF) ? 1u : 0u;
-    return cnt;
-}
-
-__global__ __launch_bounds__(256) void k_ffcount(uint32_t* __restrict__ packed,
-                                                 const unsigned long long* __restrict__ total_bits, Geom g,
-                                                 uint32_t* __restrict__ seg_ff, unsigned long long* __restrict__ super_ff) {
-    __shared__ uint32_t sWave[4];
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.y;
-    const ScanBytes s = scan_bytes(total_bits[frame]);
-    if (s.nbytes > (unsigned long long)g.packed_words * 4) return;
-    uint8_t* pb = reinterpret_cast<uint8_t*>(packed + (size_t)frame * g.packed_words);
-    for (unsigned seg = blockIdx.x; seg < s.nseg; seg += gridDim.x) {
-        uint8_t v[16];
-        const uint32_t cnt = wave_sum_u32(load16(pb, s, seg, tid, v, false));
-        if (lane == 0) sWave[wave] = cnt;
-        __syncthreads();
-        if (tid == 0) {
-            const uint32_t tot = sWave[0] + sWave[1] + sWave[2] + sWave[3];
-            seg_ff[(size_t)frame * g.nseg_cap + seg] = tot;
-            if (tot) atomicAdd(&super_ff[(size_t)frame * g.nsuper_seg + seg / kSuper], (unsigned long long)tot);
-        }
         __syncthreads();
     }
+    DMMT_TRACE(2);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint32_t v = wave_sum_u32(ff[r]);
+        if (lane == 0 && v) atomicAdd(&sFF[r], v);
+    }
+    __syncthreads();
+    if (tid < 8) chunk_ff[cid * 8 + tid] = sFF[tid];
+    if (tid == 0) {
+        chunk_bits[cid] = total;
+        const uint32_t first16 = sEdge[0] >> 16;
+        uint32_t last16;
+        if (total >= 16)
+            last16 = bits16_at(sEdge[1], sEdge[2], (int)(total - 16));
+        else
+            last16 = total ? sEdge[0] >> (32 - total) : 0u;
+        chunk_edge[cid] = (first16 << 16) | last16;
+    }
+    DMMT_TRACE(3);
+    DMMT_TRACE_FLUSH(0);
 }
 
-__global__ __launch_bounds__(256) void k_stuffwrite(uint32_t* __restrict__ packed,
+// The byte that starts m1 (1..7) bits before the end of a chunk: those last m1
+// bits of the chunk, then the next chunk's first bits, then 1-bits where the scan
+// ends (binary_stream.rs:89-96).
+__device__ __forceinline__ uint32_t boundary_byte(int m1, uint32_t last16, bool has_next, uint32_t n_next,
+                                                  uint32_t first16_next) {
+    uint32_t v = last16 & ((1u << m1) - 1u);
+    int m2 = 8 - m1;
+    if (has_next) {
+        const int t = (int)min((uint32_t)m2, n_next);
+        v = (v << t) | (t ? first16_next >> (16 - t) : 0u);
+        m2 -= t;
+    }
+    return ((v << m2) | ((1u << m2) - 1u)) & 0xFFu;
+}
+
+// 0xFF bytes whose first bit lies in chunk c (starting at scan bit b0): the
+// interior ones at the chunk's alignment + the byte it shares with the next chunk.
+__device__ __forceinline__ uint32_t chunk_ff_count(const uint32_t* __restrict__ cff, const uint32_t* __restrict__ cbits,
+                                                   const uint32_t* __restrict__ cedge, int nch, int c,
+                                                   unsigned long long b0) {
+    const uint32_t n = cbits[c];
+    const unsigned long long e = b0 + n;
+    uint32_t ffc = cff[(size_t)c * 8 + ((8 - (b0 & 7)) & 7)];
+    if ((e & 7) && (e & ~7ull) >= b0) {
+        const bool has_next = c + 1 < nch;
+        const uint32_t byte = boundary_byte((int)(e & 7), cedge[c] & 0xFFFFu, has_next, has_next ? cbits[c + 1] : 0u,
+                                            has_next ? cedge[c + 1] >> 16 : 0u);
+        ffc += byte == 0xFFu ? 1u : 0u;
+    }
+    return ffc;
+}
+
+// workgroup (1024 threads) exclusive scan; *tot receives the total
+__device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long v, unsigned long long* sWave,
+                                                              unsigned long long* tot) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    const unsigned long long incl = wave_incl_scan_u64(v);
+    if (lane == 63) sWave[wave] = incl;
+    __syncthreads();
+    unsigned long long pre = incl - v, all = 0;
+    for (int q = 0; q < 16; ++q) {
+        if (q < wave) pre += sWave[q];
+        all += sWave[q];
+    }
+    __syncthreads();
+    *tot = all;
+    return pre;
+}
+
+// -------------------------------------------------------------------- k_offsets
+__global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ chunk_bits,
+                                                  const uint32_t* __restrict__ chunk_ff,
+                                                  const uint32_t* __restrict__ chunk_edge, Geom g,
+                                                  unsigned long long* __restrict__ chunk_bit0,
+                                                  uint32_t* __restrict__ chunk_ffpre,
+                                                  unsigned long long* __restrict__ total_bits,
+                                                  unsigned long long* __restrict__ total_ff) {
+    __shared__ unsigned long long sWave[16];
+    const int tid = threadIdx.x;
+    const int frame = blockIdx.x;
+    const int nch = g.nch;
+    const uint32_t* cbits = chunk_bits + (size_t)frame * nch;
+    const uint32_t* cff = chunk_ff + (size_t)frame * nch * 8;
+    const uint32_t* cedge = chunk_edge + (size_t)frame * nch;
+    unsigned long long* bit0 = chunk_bit0 + (size_t)frame * nch;
+    uint32_t* ffpre = chunk_ffpre + (size_t)frame * nch;
+    const int per = (nch + 1023) / 1024;
+    const int c0 = min(tid * per, nch), c1 = min(c0 + per, nch);
+
+    unsigned long long mine = 0, tb = 0, tf = 0;
+    for (int c = c0; c < c1; ++c) mine += cbits[c];
+    const unsigned long long run0 = block_scan_1024(mine, sWave, &tb);
+    unsigned long long run = run0, ffsum = 0;
+    for (int c = c0; c < c1; ++c) {
+        bit0[c] = run;
+        ffsum += chunk_ff_count(cff, cbits, cedge, nch, c, run);
+        run += cbits[c];
+    }
+    unsigned long long frun = block_scan_1024(ffsum, sWave, &tf);
+    run = run0;
+    for (int c = c0; c < c1; ++c) {
+        ffpre[c] = (uint32_t)frun;
+        frun += chunk_ff_count(cff, cbits, cedge, nch, c, run);
+        run += cbits[c];
+    }
+    if (tid == 0) {
+        total_bits[frame] = tb;
+        total_ff[frame] = tf;
+    }
+}
+
+// ----------------------------------------------------------------- k_stuffwrite
+__global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__ stage,
+                                                    const uint32_t* __restrict__ chunk_bits,
+                                                    const uint32_t* __restrict__ chunk_edge,
+                                                    const unsigned long long* __restrict__ chunk_bit0,
+                                                    const uint32_t* __restrict__ chunk_ffpre,
                                                     const unsigned long long* __restrict__ total_bits,
+                                                    const unsigned long long* __restrict__ total_ff,
                                                     const uint32_t* __restrict__ hdr_len, Geom g,
-                                                    const uint32_t* __restrict__ seg_ff,
-                                                    const unsigned long long* __restrict__ super_ff,
                                                     uint8_t* __restrict__ out, size_t out_stride,
                                                     uint32_t* __restrict__ out_len, int* __restrict__ status) {
     __shared__ uint32_t sWave[4];
-    __shared__ unsigned long long sBase;
-    __shared__ uint8_t sOut[2 * kStuffSeg];
+    __shared__ uint8_t sOut[2 * kStuffPass];
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
-    const ScanBytes s = scan_bytes(total_bits[frame]);
+    const int c = blockIdx.x;
+    const size_t cid = (size_t)frame * g.nch + c;
     const uint32_t hdr = hdr_len[frame];
-    const bool fits = s.nbytes <= (unsigned long long)g.packed_words * 4 && hdr + 2 * s.nbytes + 2 <= out_stride;
-    if (!fits) {
-        if (blockIdx.x == 0 && tid == 0) {
+    const unsigned long long scan_bytes = (total_bits[frame] + 7) >> 3;
+    const unsigned long long end = (unsigned long long)hdr + scan_bytes + total_ff[frame];
+    if (end + 2 > out_stride) {  // uniform over the frame
+        if (c == 0 && tid == 0) {
             out_len[frame] = 0;  // reported as DMMT_E_CAPACITY by the host
             atomicOr(status, 16);
         }
         return;
     }
-    uint8_t* pb = reinterpret_cast<uint8_t*>(packed + (size_t)frame * g.packed_words);
-    uint8_t* o = out + (size_t)frame * out_stride + hdr;
-    for (unsigned seg = blockIdx.x; seg < s.nseg; seg += gridDim.x) {
+    const bool last = c == g.nch - 1;
+    if (last && tid == 0) {  // EOI (encoder.rs:131) and the file size
+        uint8_t* of = out + (size_t)frame * out_stride;
+        of[end] = 0xFF;
+        of[end + 1] = 0xD9;
+        out_len[frame] = (uint32_t)(end + 2);
+    }
+    const unsigned long long b0 = chunk_bit0[cid];
+    const uint32_t n = chunk_bits[cid];
+    const unsigned long long e = b0 + n;
+    const unsigned long long kbeg = (b0 + 7) >> 3, kend = (e + 7) >> 3;
+    if (kend <= kbeg) return;  // a tail chunk inside the previous chunk's last byte
+    const unsigned long long nbytes = kend - kbeg;
+    // the chunk's last byte, when shared with the next chunk or the padding
+    const bool shared_tail = (e & 7) != 0;
+    uint32_t tail = 0;
+    if (shared_tail) {
+        const bool has_next = !last;
+        tail = boundary_byte((int)(e & 7), chunk_edge[cid] & 0xFFFFu, has_next, has_next ? chunk_bits[cid + 1] : 0u,
+                             has_next ? chunk_edge[cid + 1] >> 16 : 0u);
+    }
+    const uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
+    const unsigned off = (unsigned)(8 * kbeg - b0);  // the first owned byte starts this many bits into the chunk
+    uint8_t* o = out + (size_t)frame * out_stride + hdr + kbeg + chunk_ffpre[cid];
+    for (unsigned long long pos = 0; pos < nbytes; pos += kStuffPass) {  // uniform
+        const unsigned long long kb = pos + 16u * (unsigned)tid;          // first of my 16 bytes (chunk-relative)
         uint8_t v[16];
-        const uint32_t cnt = load16(pb, s, seg, tid, v, true);
+        uint32_t cnt = 0;
+        if (kb < nbytes) {
+            const unsigned long long p = off + 8 * kb;  // bit position in the chunk stream
+            const size_t wi = (size_t)(p >> 5);
+            const int sh = (int)(p & 31);
+            uint32_t wv[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) wv[i] = slot[wi + i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t x = sh ? (wv[i] << sh) | (wv[i + 1] >> (32 - sh)) : wv[i];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[4 * i + j] = (uint8_t)(x >> (24 - 8 * j));
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (shared_tail && kb + j == nbytes - 1) v[j] = (uint8_t)tail;
+                cnt += (kb + j < nbytes && v[j] == 0xFF) ? 1u : 0u;
+            }
+        }
         const uint32_t incl = wave_incl_scan_u32(cnt);
         if (lane == 63) sWave[wave] = incl;
-        if (wave == 0) {
-            const unsigned long long pre = prefix_two_level(super_ff + (size_t)frame * g.nsuper_seg,
-                                                            seg_ff + (size_t)frame * g.nseg_cap, seg);
-            if (lane == 0) sBase = pre;
-        }
         __syncthreads();
-        // stage the stuffed segment in LDS, then store it with consecutive lanes on
+        uint32_t pre = incl - cnt;
+        for (int q = 0; q < wave; ++q) pre += sWave[q];
+        const uint32_t ffs = sWave[0] + sWave[1] + sWave[2] + sWave[3];
+        // stage the stuffed pass in LDS, then store it with consecutive lanes on
         // consecutive bytes (coalesced)
-        uint32_t pre = 0;
-        for (int w = 0; w < wave; ++w) pre += sWave[w];
-        uint32_t dst = (uint32_t)tid * 16u + pre + (incl - cnt);
-        const unsigned long long b0 = (unsigned long long)seg * kStuffSeg + (unsigned)tid * 16u;
+        if (kb < nbytes) {
+            uint32_t dst = (uint32_t)tid * 16u + pre;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (b0 + j < s.nbytes) {
-                sOut[dst++] = v[j];
-                if (v[j] == 0xFF) sOut[dst++] = 0x00;
+            for (int j = 0; j < 16; ++j) {
+                if (kb + j < nbytes) {
+                    sOut[dst++] = v[j];
+                    if (v[j] == 0xFF) sOut[dst++] = 0x00;
+                }
             }
         }
         __syncthreads();
-        const unsigned long long seg0 = (unsigned long long)seg * kStuffSeg;
-        const unsigned long long in_seg = s.nbytes - seg0 < (unsigned long long)kStuffSeg ? s.nbytes - seg0 : kStuffSeg;
-        const uint32_t ffs = sWave[0] + sWave[1] + sWave[2] + sWave[3];
-        const uint32_t seg_len = (uint32_t)in_seg + ffs;
-        uint8_t* od = o + seg0 + sBase;
-        for (uint32_t i = (uint32_t)tid; i < seg_len; i += 256) od[i] = sOut[i];
-        if (tid == 0 && seg == s.nseg - 1) {  // EOI (encoder.rs:131) and the file size
-            const unsigned long long total = (unsigned long long)hdr + s.nbytes + sBase + ffs;
-            uint8_t* of = out + (size_t)frame * out_stride;
-            of[total] = 0xFF;
-            of[total + 1] = 0xD9;
-            out_len[frame] = (uint32_t)(total + 2);
-        }
-        __syncthreads();  // sWave / sBase / sOut reuse
+        const unsigned long long in_pass = nbytes - pos < (unsigned long long)kStuffPass ? nbytes - pos : kStuffPass;
+        const uint32_t len = (uint32_t)in_pass + ffs;
+        for (uint32_t i = (uint32_t)tid; i < len; i += 256) o[i] = sOut[i];
+        o += len;
+        __syncthreads();  // sWave / sOut reuse
     }
 }
 
 // --------------------------------------------------------------------- launchers
-hipError_t launch_bits(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
-    hipLaunchKernelGGL(k_bits, dim3(g.nch, n_frames), dim3(256), 0, st, (const int16_t*)w.coef,
-                       (const int16_t*)w.dcdiff, (const uint32_t*)w.code_tab, g, w.block_bits, w.chunk_bits,
-                       w.super_bits, w.ac_hist, w.dc_hist);
+hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
+    hipLaunchKernelGGL(k_emit, dim3(g.nch, n_frames), dim3(256), 0, st, (const int16_t*)w.coef,
+                       (const int16_t*)w.dcdiff, (const uint32_t*)w.code_tab, g, w.stage, w.chunk_bits, w.chunk_ff,
+                       w.chunk_edge, w.ac_hist, w.dc_hist);
     return hipGetLastError();
 }
 
-hipError_t launch_place(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
-    hipLaunchKernelGGL(k_place, dim3(g.nch, n_frames), dim3(256), 0, st, (const int16_t*)w.coef,
-                       (const int16_t*)w.dcdiff, (const uint32_t*)w.code_tab, g, (const uint16_t*)w.block_bits,
-                       (const uint32_t*)w.chunk_bits, (const unsigned long long*)w.super_bits, w.total_bits, w.packed,
-                       w.status);
-    return hipGetLastError();
-}
-
-static int seg_grid(const Geom& g, int n_frames) {
-    int per_frame = 2048 / n_frames;
-    if (per_frame < 1) per_frame = 1;
-    const int cap = g.nseg_cap < 1 ? 1 : g.nseg_cap;
-    return cap < per_frame ? cap : per_frame;
-}
-
-hipError_t launch_ffcount(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
-    hipLaunchKernelGGL(k_ffcount, dim3(seg_grid(g, n_frames), n_frames), dim3(256), 0, st, w.packed,
-                       (const unsigned long long*)w.total_bits, g, w.seg_ff, w.super_ff);
+hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
+    hipLaunchKernelGGL(k_offsets, dim3(n_frames), dim3(1024), 0, st, (const uint32_t*)w.chunk_bits,
+                       (const uint32_t*)w.chunk_ff, (const uint32_t*)w.chunk_edge, g, w.chunk_bit0, w.chunk_ffpre,
+                       w.total_bits, w.total_ff);
     return hipGetLastError();
 }
 
 hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
                              uint32_t* out_len, hipStream_t st) {
-    hipLaunchKernelGGL(k_stuffwrite, dim3(seg_grid(g, n_frames), n_frames), dim3(256), 0, st, w.packed,
-                       (const unsigned long long*)w.total_bits, (const uint32_t*)w.hdr_len, g,
-                       (const uint32_t*)w.seg_ff, (const unsigned long long*)w.super_ff, out, out_stride, out_len,
-                       w.status);
+    hipLaunchKernelGGL(k_stuffwrite, dim3(g.nch, n_frames), dim3(256), 0, st, (const uint32_t*)w.stage,
+                       (const uint32_t*)w.chunk_bits, (const uint32_t*)w.chunk_edge,
+                       (const unsigned long long*)w.chunk_bit0, (const uint32_t*)w.chunk_ffpre,
+                       (const unsigned long long*)w.total_bits, (const unsigned long long*)w.total_ff,
+                       (const uint32_t*)w.hdr_len, g, out, out_stride, out_len, w.status);
     return hipGetLastError();
 }
 

@@ -14,15 +14,13 @@ static constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 
 // Histogram replicas per frame: the front/DC kernels add their per-workgroup
 // histograms into replica (blockIdx.x % kHistReps) to spread atomic traffic.
 static constexpr int kHistReps = 16;
-// Blocks per entropy chunk (k_bits / k_place): one workgroup each.
+// Blocks per entropy chunk (k_emit / k_stuffwrite): one workgroup each.
 static constexpr int kChunkBlocks = 256;
 // Worst-case entropy-coded bits of one block: DC code 16 + 12 extra bits, 63 AC
 // tokens of code 16 + 12 extra bits (|coef| <= 2048 for 8-bit-range input).
 static constexpr int kMaxBlockBits = 28 * 64;
-// Chunks (or stuffing segments) per "super" counter of the two-level offsets.
-static constexpr int kSuper = 64;
-// Bytes per segment of the byte-stuffing pass.
-static constexpr int kStuffSeg = 4096;
+// Staging words of one chunk's bit stream (worst case).
+static constexpr long long kChunkWordsCap = (long long)kChunkBlocks * kMaxBlockBits / 32;
 // Upper bound of the header the table kernel writes (SOI..SOS incl. DRI).
 static constexpr int kMaxHeaderBytes = 2 + 18 + 2 * 69 + 19 + 4 * (4 + 17 + 256) + 6 + 14;
 
@@ -37,10 +35,7 @@ struct Geom {
     int restart_interval;   // 0 = reference behaviour
     long long bpf;          // blocks per frame
     int nch;                // entropy chunks per frame
-    int nsuper;             // super counters over the chunks
-    int nseg_cap;           // stuffing segments per frame (capacity)
-    int nsuper_seg;         // super counters over the segments
-    long long packed_words; // words of the packed-bit buffer per frame
+    long long max_scan_bytes;  // worst-case entropy-coded bytes per frame (before stuffing)
 };
 
 inline Geom make_geom(int width, int height, int subsampling, int maxval, int restart_interval) {
@@ -60,18 +55,13 @@ inline Geom make_geom(int width, int height, int subsampling, int maxval, int re
     g.restart_interval = restart_interval;
     g.bpf = (long long)g.nmcu * g.bpm;
     g.nch = (int)((g.bpf + kChunkBlocks - 1) / kChunkBlocks);
-    g.nsuper = (g.nch + kSuper - 1) / kSuper;
-    long long max_bits = g.bpf * kMaxBlockBits + 8LL * g.nmcu; // + restart padding
-    g.packed_words = ((max_bits + 31) / 32 + 2 + 63) / 64 * 64;  // 256-byte aligned frame regions
-    long long max_bytes = g.packed_words * 4;
-    g.nseg_cap = (int)((max_bytes + kStuffSeg - 1) / kStuffSeg);
-    g.nsuper_seg = (g.nseg_cap + kSuper - 1) / kSuper;
+    g.max_scan_bytes = (g.bpf * kMaxBlockBits + 7) / 8;
     return g;
 }
 
 // Worst-case JPEG size: header + every scan byte stuffed + RST markers + EOI.
 inline size_t max_jpeg_bytes(const Geom& g) {
-    return (size_t)kMaxHeaderBytes + (size_t)g.packed_words * 4 * 2 + 2 * (size_t)g.nmcu + 2 + 64;
+    return (size_t)kMaxHeaderBytes + (size_t)g.max_scan_bytes * 2 + 2 * (size_t)g.nmcu + 2 + 64;
 }
 
 }  // namespace dmmt

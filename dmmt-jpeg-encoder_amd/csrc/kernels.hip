@@ -15,8 +15,8 @@
 //               codes, JFIF header bytes [symbol_counting.rs:85-94,
 //               length_limited.rs:37-134, huffman/encoder.rs:45-157,
 //               encoder.rs:125-262]
-//  k_bits, k_place, k_ffcount, k_stuffwrite (entropy.hip): bit packing at
-//               exact offsets, byte stuffing, EOI [encoder.rs:264-404,
+//  k_emit, k_offsets, k_stuffwrite (entropy.hip): Huffman bit emission per
+//               chunk, chunk offsets, byte stuffing, EOI [encoder.rs:264-404,
 //               binary_stream.rs:38-96, segment_marker_injector.rs:13-30]
 //
 // Floating point: this file is compiled with -ffp-contract=off and without
@@ -443,20 +443,13 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
 // DC difference per component in emission order (categorize.rs:153-169), with
 // the predictor reset at restart-interval starts (extension), + DC histograms.
 __global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, int16_t* __restrict__ dcdiff, Geom g,
-                                                uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
-                                                unsigned long long* __restrict__ super_bits,
-                                                unsigned long long* __restrict__ super_ff) {
+                                                uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/) {
     __shared__ uint32_t sH[32];
     const int tid = threadIdx.x;
     const int frame = blockIdx.y;
     if (tid < 32) sH[tid] = 0;
     __syncthreads();
     const long long base = (long long)frame * g.bpf;
-    // reset the super counters k_bits / k_ffcount add into in this launch
-    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nsuper; i += (long long)gridDim.x * 256)
-        super_bits[(size_t)frame * g.nsuper + i] = 0ull;
-    for (long long i = (long long)blockIdx.x * 256 + tid; i < g.nsuper_seg; i += (long long)gridDim.x * 256)
-        super_ff[(size_t)frame * g.nsuper_seg + i] = 0ull;
     for (long long el = (long long)blockIdx.x * 256 + tid; el < g.bpf; el += (long long)gridDim.x * 256) {
         const int m = (int)(el / g.bpm);
         const int k = (int)(el - (long long)m * g.bpm);
@@ -480,7 +473,7 @@ __global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, 
 // One 512-thread workgroup per (table, frame): blockIdx.x = table (0 luma DC,
 // 1 luma AC, 2 chroma DC, 3 chroma AC); thread s < 256 = symbol / leaf s,
 // thread 256 + j = package j.
-//  1 histograms summed over the replicas (k_bits zeroes them after this launch);
+//  1 histograms summed over the replicas (k_emit zeroes them after this launch);
 //    every workgroup counts the present symbols of all four tables, which place
 //    the DHT segments
 //  2 compact the present symbols and rank them by (frequency, symbol): the stable
@@ -962,8 +955,7 @@ hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_
 hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
     const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
-    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist, w.super_bits,
-                       w.super_ff);
+    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist);
     return hipGetLastError();
 }
 

@@ -17,19 +17,20 @@ struct Work {
     uint32_t* code_tab;             // [frames][4][256]  (len << 16) | code
     uint32_t* hdr_len;              // [frames]
     unsigned long long* total_bits; // [frames]
-    uint32_t* packed;               // [frames][packed_words], all zero between launches
-    uint16_t* block_bits;           // [frames][bpf] entropy-coded bits per block
-    uint32_t* chunk_bits;           // [frames][nch]
-    unsigned long long* super_bits; // [frames][nsuper], zeroed by k_dcdiff
-    uint32_t* seg_ff;               // [frames][nseg_cap] 0xFF bytes per stuffing segment
-    unsigned long long* super_ff;   // [frames][nsuper_seg], zeroed by k_dcdiff
-    int* status;                    // error bits: 1 value>max, 2 table, 8/16 capacity
+    uint32_t* stage;                // [frames][nch][kChunkWordsCap] each chunk's own bit stream, MSB first
+    uint32_t* chunk_bits;           // [frames][nch] bits of the chunk
+    uint32_t* chunk_ff;             // [frames][nch][8] 0xFF bytes inside the chunk per alignment residue
+    uint32_t* chunk_edge;           // [frames][nch] first 16 bits << 16 | last 16 bits
+    unsigned long long* chunk_bit0; // [frames][nch] bit offset of the chunk in the scan
+    uint32_t* chunk_ffpre;          // [frames][nch] 0xFF bytes in the scan before the chunk's bytes
+    unsigned long long* total_ff;   // [frames] 0xFF bytes of the scan
+    int* status;                    // error bits: 1 value>max, 2 table, 16 output capacity
     const float* norm_lut;          // maxval-normalisation table
     const float* qtab;              // [2][64] f32
     const uint8_t* qtab_u8;         // [2][64]
 };
 
-enum Stage { ST_FRONT = 0, ST_DCDIFF, ST_TABLES, ST_BITS, ST_PLACE, ST_FFCOUNT, ST_STUFFWRITE, ST_AC_HIST, ST_COUNT };
+enum Stage { ST_FRONT = 0, ST_DCDIFF, ST_TABLES, ST_EMIT, ST_OFFSETS, ST_STUFFWRITE, ST_AC_HIST, ST_COUNT };
 
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
                         const Work& w, hipStream_t st);
@@ -37,9 +38,8 @@ hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_
 hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st);
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st);
-hipError_t launch_bits(int n_frames, const Geom& g, const Work& w, hipStream_t st);
-hipError_t launch_place(int n_frames, const Geom& g, const Work& w, hipStream_t st);
-hipError_t launch_ffcount(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_t st);
 hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
                              uint32_t* out_len, hipStream_t st);
 hipError_t launch_dct_blocks(float* data, long long nblocks, hipStream_t st);
