@@ -1,0 +1,100 @@
+"""The N>1 bench path on CPU: two ranks over gloo, a stand-in encoder.
+
+bench.py's multi-GPU contract: every rank encodes its own
+frames (independent images, weak scaling, no data-path collective); the timed
+region is bracketed by barriers; the elapsed time is the MAX over ranks; rank 0
+prints one JSON line whose `value` is the whole-job pixel rate.  The stand-in
+encoder records which synthetic frames each rank generated and sleeps a
+rank-dependent time per step so the MAX reduction is observable.
+"""
+import json
+import os
+import socket
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dmmt-jpeg-encoder_amd"))
+
+STEP_SLEEP = {0: 0.001, 1: 0.004}  # rank 1 is the slow one
+
+
+class StandInEncoder:
+    def __init__(self, local_rank, rank, log):
+        self.rank, self.log = rank, log
+        self.mem = {}
+        self.mask = 0
+
+    def malloc(self, n):
+        h = len(self.mem) + 1
+        self.mem[h] = n
+        return h
+
+    def free(self, h):
+        self.mem.pop(h, None)
+
+    def fill_synthetic(self, d, w, h, n_frames, first_frame=0, seed=0x9E3779B9):
+        self.log.append(("frames", self.rank, first_frame, n_frames))
+
+    def encode_device(self, d_in, n, w, h, opts, d_out, out_stride, d_len, frame_stride=0, opt_c=None):
+        time.sleep(STEP_SLEEP[self.rank])
+
+    def synchronize(self):
+        pass
+
+    def set_profiling(self, mask):
+        self.mask = mask
+
+    def profile(self):
+        return {"front": (0.05 * 3, 3)}
+
+    def d2h(self, d, n):
+        return np.full(n // 4, 1000, np.uint32).tobytes()
+
+    def close(self):
+        pass
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import bench
+    log, lines = [], []
+    bench.main(["--gpus", str(world), "--steps", "20", "--warmup", "2", "--cpu-seconds", "0",
+                "--config", "1080p420q75x256"],
+               make_encoder=lambda lr: StandInEncoder(lr, rank, log), emit=lines.append)
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump({"log": log, "lines": lines}, f)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_gloo(tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn")
+    r0 = json.load(open(tmp_path / "rank0.json"))
+    r1 = json.load(open(tmp_path / "rank1.json"))
+    assert len(r0["lines"]) == 1 and r1["lines"] == []  # one JSON line, rank 0 only
+    line = json.loads(r0["lines"][0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["steps"] == 20
+    # distinct synthetic frames per rank (no two ranks encode the same frames)
+    f0 = {tuple(x[2:]) for x in r0["log"]}
+    f1 = {tuple(x[2:]) for x in r1["log"]}
+    assert f0 and f1 and not (f0 & f1)
+    # elapsed is the MAX over ranks: at least the slow rank's sleeps
+    assert line["ms_per_step"] >= STEP_SLEEP[1] * 1e3 * 0.9
+    # value = whole-job pixels / elapsed
+    w, h, fps = 1920, 1080, 256
+    expect = w * h * fps * 20 * world / (line["ms_per_step"] * 20 / 1e3) / 1e6
+    assert line["value"] == pytest.approx(expect, rel=2e-3)
+    assert line["config"]["parallelism"] == "independent frames x2"
