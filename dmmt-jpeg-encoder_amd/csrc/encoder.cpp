@@ -140,6 +140,10 @@ int upload_tables(dmmt_ctx* c, const dmmt_options* opt, int maxval, int sb, hipS
         memcpy(c->q_cached, q, 128);
         c->q_valid = true;
     }
+    if (sb == 4) {  // Image<f32> input: already normalised, no table
+        if (!c->lut.p && (rc = ensure(c->lut, 256 * sizeof(float)))) return rc;
+        return DMMT_OK;
+    }
     if (c->lut_maxval != maxval || c->lut_sb != sb) {
         const size_t n = sb == 1 ? 256 : 65536;
         if ((rc = ensure(c->lut, n * sizeof(float)))) return rc;
@@ -438,7 +442,7 @@ extern "C" int dmmt_encode_device(dmmt_ctx* c, const dmmt_device_frames* f, cons
     int rc;
     if ((rc = validate(opt))) return rc;
     if (f->n_frames <= 0 || !f->d_rgb || !f->d_out || !f->d_out_len) return DMMT_E_INVALID_ARGUMENT;
-    if (f->sample_bytes != 1 && f->sample_bytes != 2) return DMMT_E_INVALID_ARGUMENT;
+    if (f->sample_bytes != 1 && f->sample_bytes != 2 && f->sample_bytes != 4) return DMMT_E_INVALID_ARGUMENT;
     Geom g;
     if ((rc = make_checked_geom(f->width, f->height, opt->subsampling, f->maxval, opt->restart_interval, &g))) return rc;
     if (f->out_stride < max_jpeg_bytes(g)) return DMMT_E_CAPACITY;
@@ -486,7 +490,7 @@ static int encode_host_group(dmmt_ctx* c, const dmmt_image* imgs, int n, const d
 
 static int check_image(const dmmt_image* img) {
     if (!img || !img->rgb) return DMMT_E_INVALID_ARGUMENT;
-    if (img->sample_bytes != 1 && img->sample_bytes != 2) return DMMT_E_INVALID_ARGUMENT;
+    if (img->sample_bytes != 1 && img->sample_bytes != 2 && img->sample_bytes != 4) return DMMT_E_INVALID_ARGUMENT;
     if (img->width == 0 || img->height == 0) return DMMT_E_INVALID_ARGUMENT;
     return DMMT_OK;
 }

@@ -248,14 +248,18 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
         if (tid < NJ) {
             const int c = tid % CB, r = tid / CB;  // chroma block, chroma row
             const int lx0 = c * 8 * HR;            // first pixel column of the job
-            uint32_t pw[VR][PXW];                  // raw bytes of the job's VR pixel rows
+            uint32_t pw[VR][SB == 4 ? 1 : PXW];    // raw bytes of the job's VR pixel rows (integer samples)
+            const float* fsrc[VR];                 // the rows themselves (float samples)
 #pragma unroll
             for (int dy = 0; dy < VR; ++dy) {
                 const int ly = r * VR + dy;
                 const long long start = Raw::row_start(g, x0, y0 + ly);
                 const int mis = Raw::misalign(fbase, start);
                 const uint8_t* src = sRaw + ly * Raw::RS + mis + lx0 * 3 * SB;
-                if ((mis & 7) == 0) {
+                fsrc[dy] = reinterpret_cast<const float*>(src);
+                if constexpr (SB == 4) {
+                    pw[dy][0] = 0u;
+                } else if ((mis & 7) == 0) {
 #pragma unroll
                     for (int k = 0; k < PXW / 2; ++k) {
                         const uint2 u = reinterpret_cast<const uint2*>(src)[k];
@@ -282,7 +286,13 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
                         const int px = x0 + lx0 + jx;
                         const int py = y0 + r * VR + dy;
                         float rr = 0.0f, gg = 0.0f, bb = 0.0f;
-                        if (px < g.width && py < g.height) {
+                        if constexpr (SB == 4) {  // Image<f32> dots as given
+                            if (px < g.width && py < g.height) {
+                                rr = fsrc[dy][jx * 3];
+                                gg = fsrc[dy][jx * 3 + 1];
+                                bb = fsrc[dy][jx * 3 + 2];
+                            }
+                        } else if (px < g.width && py < g.height) {
                             uint32_t sv[3];
 #pragma unroll
                             for (int ch = 0; ch < 3; ++ch) {
@@ -928,7 +938,14 @@ static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
                         const Work& w, hipStream_t st) {
     const size_t se = frame_stride_bytes / (size_t)sample_bytes;
-    if (sample_bytes == 1) {
+    if (sample_bytes == 4) {
+        if (g.hr == 1)
+            front_impl<1, 1, float>(rgb, se, n_frames, g, w, st);
+        else if (g.vr == 1)
+            front_impl<2, 1, float>(rgb, se, n_frames, g, w, st);
+        else
+            front_impl<2, 2, float>(rgb, se, n_frames, g, w, st);
+    } else if (sample_bytes == 1) {
         if (g.hr == 1)
             front_impl<1, 1, uint8_t>(rgb, se, n_frames, g, w, st);
         else if (g.vr == 1)

@@ -223,18 +223,21 @@ class JpegTransformationOptions:
 
 @dataclass
 class Image:
-    """Image (src/image.rs:7-11) kept as raw samples + maxval; the GPU applies
-    ``v as f32 / max as f32`` (color.rs:45-53)."""
+    """Image (src/image.rs:7-11).  Integer samples are kept raw with their maxval
+    and the GPU applies ``v as f32 / max as f32`` (color.rs:45-53); float32
+    samples are the reference's Image<f32> dots, already normalised."""
     width: int
     height: int
     maxval: int
-    samples: np.ndarray  # (height, width, 3) uint8 or uint16
+    samples: np.ndarray  # (height, width, 3) uint8, uint16 or float32
 
     @classmethod
     def from_array(cls, rgb, maxval: int = 255) -> "Image":
         a = np.asarray(rgb)
         if a.ndim != 3 or a.shape[2] != 3:
             raise ValueError("rgb must be (height, width, 3)")
+        if a.dtype == np.float32:
+            return cls(a.shape[1], a.shape[0], int(maxval), np.ascontiguousarray(a))
         dt = np.uint8 if maxval <= 255 and (a.size == 0 or a.max() <= 255) else np.uint16
         return cls(a.shape[1], a.shape[0], int(maxval), np.ascontiguousarray(a, dtype=dt))
 

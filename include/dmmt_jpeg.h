@@ -73,10 +73,13 @@ enum dmmt_quant_preset {
     DMMT_Q_AN_IMPROVED_DETECTION_MODEL = 6
 };
 
-/* Image<f32> (image.rs:7-11) before normalisation: the raw PPM samples and maxval
- * (ppm.rs:145-163); the library reproduces `v as f32 / max as f32` (color.rs:45-53)
- * on the device.  rgb is interleaved R,G,B, row-major, sample_bytes 1 (uint8) or 2
- * (uint16, host endian). */
+/* Image<f32> (image.rs:7-11).  Either before normalisation -- the raw PPM samples
+ * and maxval (ppm.rs:145-163), sample_bytes 1 (uint8) or 2 (uint16, host endian);
+ * the library reproduces `v as f32 / max as f32` (color.rs:45-53) on the device and
+ * reports a sample above maxval (color.rs:63-65) -- or exactly the reference's
+ * Image<f32> dots: sample_bytes 4, float R,G,B already normalised (maxval unused),
+ * the form JpegImageWriter (jpeg.rs:48-75) receives.  rgb is interleaved R,G,B,
+ * row-major. */
 typedef struct dmmt_image {
     uint16_t width;
     uint16_t height;
@@ -100,7 +103,7 @@ typedef struct dmmt_device_frames {
     const void* d_rgb;          /* n_frames frames, frame f at d_rgb + f * frame_stride */
     size_t frame_stride;        /* bytes between frames */
     int32_t n_frames;
-    uint16_t width, height, maxval, sample_bytes;
+    uint16_t width, height, maxval, sample_bytes; /* as dmmt_image */
     uint8_t* d_out;             /* JPEG f written at d_out + f * out_stride */
     size_t out_stride;          /* >= dmmt_max_jpeg_bytes(width, height, subsampling) */
     uint32_t* d_out_len;        /* device array [n_frames] of JPEG sizes */

@@ -110,6 +110,20 @@ def test_16bit_and_odd_maxval(encoder, spec_tables, maxval):
         assert encoder.encode(img, opts(sub, *spec_tables)) == oracle.encode(rgb, maxval, sub, *spec_tables)
 
 
+@pytest.mark.parametrize("sub", SUBS)
+@pytest.mark.parametrize("shape", [(1, 1), (9, 13), (16, 16), (61, 203), (270, 480)])
+def test_image_f32_input(encoder, spec_tables, sub, shape):
+    """sample_bytes 4: the reference's Image<f32> dots (`v as f32 / max as f32`,
+    color.rs:45-53, computed here in float32) -- the JpegImageWriter seam."""
+    h, w = shape
+    rgb = synthetic(w, h, frame=w)
+    for maxval in (255, 1000):
+        raw = rgb.astype(np.uint16) * (maxval // 255)
+        f32 = raw.astype(np.float32) / np.float32(maxval)
+        gpu = encoder.encode(dmmt_jpeg.Image.from_array(f32, maxval), opts(sub, *spec_tables))
+        assert gpu == oracle.encode(raw, maxval, sub, *spec_tables)
+
+
 def test_value_above_maxval_is_an_error(encoder, spec_tables):
     rgb = np.full((8, 8, 3), 200, np.uint8)
     with pytest.raises(dmmt_jpeg.Error) as e:
