@@ -54,6 +54,20 @@ __device__ __forceinline__ int16_t quantize(float d, float q) {
     return (int16_t)(int)x;
 }
 
+// The same result as quantize(d, q) without the division in the common case:
+// t = d * (1/q) is within 1.5 * 2^-23 |d/q| of the correctly rounded quotient, so
+// round(t) == round(fl(d/q)) unless t lies within that distance of a
+// half-integer (or is huge / not finite); only those lanes divide.
+__device__ __forceinline__ int16_t quantize_rcp(float d, float q, float rq) {
+    float t = d * rq;
+    const float a = fabsf(t);
+    if (!(a < 4194304.0f) || !(fabsf((a - floorf(a)) - 0.5f) > a * 0x1p-20f)) t = d / q;
+    float x = roundf(t);
+    if (x != x) return 0;
+    x = fminf(fmaxf(x, -32768.0f), 32767.0f);
+    return (int16_t)(int)x;
+}
+
 // arai.rs:7-26 constants, f32 literals as written in the reference
 #define DMMT_A1 0.70710678118654752440f
 #define DMMT_A2 0.5411961f
@@ -93,17 +107,6 @@ __device__ __forceinline__ void rgb_to_ycbcr(float r, float g, float b, float& y
 }
 
 // ============================================================== k_front
-//
-// One workgroup (256 threads) per tile = TM horizontally adjacent MCUs of one
-// MCU row (256 padded pixel columns, 8*VR rows), grid-strided over the frame's
-// tiles; blockIdx.y = frame.
-//  A  pixels -> YCbCr in LDS; chroma box-averaged in the reference's sum order
-//  B  row DCT: one lane per (block, row), in place in LDS
-//  C  column DCT + quantise: one lane per (block, column) -> zigzag int16 in LDS,
-//     laid out in local MCU emission order
-//  D  coalesced 16-byte stores of the tile's blocks + DC values
-//  E  AC symbols: one wave per block, lane = zigzag position, ballot finds the
-//     previous non-zero coefficient; LDS histogram, flushed once per workgroup.
 
 // Raw pixel staging: a tile row is 256 pixels = RB bytes, fetched as the RC
 // aligned 16-byte chunks that cover it at any alignment (byte loads only for a
@@ -167,12 +170,12 @@ struct RawTile {
 //     block) converts its 8*HR x VR pixels (raw bytes from LDS), box-averages the
 //     chroma in the reference's sum order and runs the row pass of the HR*VR luma
 //     rows and the two chroma rows in registers -> block-major LDS (stride BS)
-//  C  column DCT + quantise: one lane per (block, column); results held in
-//     registers across a barrier, then scattered in zigzag order into the
+//  C  column DCT + quantise (quantize_rcp): one lane per (block, column); results
+//     held in registers across a barrier, then scattered in zigzag order into the
 //     (aliased) int16 block image in local MCU emission order
-//  D  coalesced 16-byte stores of the tile's blocks + DC values
-//  E  AC symbols: one wave per block, lane = zigzag position, ballot finds the
-//     previous non-zero coefficient; LDS histogram, flushed once per workgroup.
+//  D  coalesced 16-byte stores of the tile's blocks + DC values (wave 3), beside
+//  E  AC symbols (waves 0-2): two threads per block walk its coefficients from
+//     registers; LDS histogram, flushed once per workgroup.
 template <int HR, int VR, typename Sample>
 __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, size_t frame_stride, Geom g,
                                                const float* __restrict__ norm_lut,
@@ -203,6 +206,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
     __shared__ uint32_t sHist[2 * 256];
     __shared__ float sLut[256];
     __shared__ float sQ[128];
+    __shared__ float sRQ[128];  // 1/q, correctly rounded
     int16_t* const sCoef = reinterpret_cast<int16_t*>(sT);
 
     DMMT_TRACE_START;
@@ -212,6 +216,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
     const long long fbytes = (long long)g.width * g.height * 3 * SB;
     for (int i = tid; i < 512; i += 256) sHist[i] = 0;
     if (tid < 128) sQ[tid] = qtab[tid];
+    if (tid < 128) sRQ[tid] = 1.0f / qtab[tid];
     if (SB == 1) sLut[tid] = norm_lut[tid];
     // the column pass always handles column tid & 7: its 8 zigzag destinations
     uint8_t zz[8];
@@ -366,10 +371,11 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = sT[blk * BS + i * 8 + col];
                 arai8(v);
+                const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    qv[jj][i] = (uint32_t)(uint16_t)quantize(v[2 * i], q[16 * i]) |
-                                ((uint32_t)(uint16_t)quantize(v[2 * i + 1], q[16 * i + 8]) << 16);
+                    qv[jj][i] = (uint32_t)(uint16_t)quantize_rcp(v[2 * i], q[16 * i], rq[16 * i]) |
+                                ((uint32_t)(uint16_t)quantize_rcp(v[2 * i + 1], q[16 * i + 8], rq[16 * i + 8]) << 16);
             }
         }
         __syncthreads();  // every column read: the int16 image may now overwrite sT
@@ -395,36 +401,57 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
         __syncthreads();
         DMMT_TRACE(2);
 
-        // ---- D + E, side by side: waves 2-3 store the tile's blocks (contiguous in
-        // emission order) and DCs; in waves 0-1 one thread per block walks its 63 AC
-        // coefficients from registers and counts the run/size symbols
+        // ---- D + E, side by side: wave 3 stores the tile's blocks (contiguous in
+        // emission order) and DCs; in waves 0-2 two threads per block walk its AC
+        // coefficients from registers and count the run/size symbols
         // (categorize.rs:132-151): ZRL per 16 zeros before a non-zero, EOB after
         // trailing zeros.
         const int nmcu_valid = min(TM, g.mcux - mx0);
         const int nblk = nmcu_valid * BPM;
         const long long e0 = (long long)frame * g.bpf + ((long long)my * g.mcux + mx0) * BPM;
-        static_assert(NB <= 128, "one symbol-walk thread per block in waves 0-1");
-        if (tid >= 128) {
+        static_assert(NB <= 96, "two symbol-walk threads per block in waves 0-2");
+        if (tid >= 192) {
             uint4* dst = reinterpret_cast<uint4*>(coef + e0 * 64);
-            for (int i = tid - 128; i < nblk * 8; i += 128)
+            for (int i = tid - 192; i < nblk * 8; i += 64)
                 dst[i] = *reinterpret_cast<const uint4*>(sCoef + (i >> 3) * CS + (i & 7) * 8);
-            for (int b = tid - 128; b < nblk; b += 128) dc[e0 + b] = sCoef[b * CS];
-        } else if (tid < nblk) {
-            uint32_t w[32];
-            const uint4* src = reinterpret_cast<const uint4*>(sCoef + tid * CS);
+            for (int b = tid - 192; b < nblk; b += 64) dc[e0 + b] = sCoef[b * CS];
+        } else if (tid < 2 * nblk) {
+            // thread pair per block: half 0 walks zigzag positions 1..31, half 1
+            // positions 32..63 starting from the zero run half 0 ends with
+            const int blk = tid >> 1, half = tid & 1;
+            uint32_t w[16];
+            const uint4* src = reinterpret_cast<const uint4*>(sCoef + blk * CS) + 4 * half;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < 4; ++i) {
                 const uint4 u = src[i];
                 w[4 * i] = u.x;
                 w[4 * i + 1] = u.y;
                 w[4 * i + 2] = u.z;
                 w[4 * i + 3] = u.w;
             }
-            uint32_t* h = sHist + ((tid % BPM) < NLUMA ? 0 : 256);
             int run = 0;
+            if (half) {  // zeros after the last non-zero of positions 1..31
+                const uint4* lo = reinterpret_cast<const uint4*>(sCoef + blk * CS);
+                uint32_t nzm = 0;  // bit k: position k non-zero
 #pragma unroll
-            for (int k = 1; k < 64; ++k) {
-                const int v = (k & 1) ? ((int)w[k >> 1] >> 16) : (int)(int16_t)(w[k >> 1] & 0xFFFFu);
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 u = lo[i];
+                    const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int k = 8 * i + 2 * j;
+                        nzm |= ((q[j] & 0xFFFFu) != 0u ? 1u : 0u) << k;
+                        nzm |= ((q[j] >> 16) != 0u ? 1u : 0u) << (k + 1);
+                    }
+                }
+                nzm &= ~1u;  // not the DC
+                run = nzm ? 31 - (31 - __clz((int)nzm)) : 31;
+            }
+            uint32_t* h = sHist + ((blk % BPM) < NLUMA ? 0 : 256);
+#pragma unroll
+            for (int kk = 0; kk < 32; ++kk) {
+                if (kk == 0 && !half) continue;  // the DC
+                const int v = (kk & 1) ? ((int)w[kk >> 1] >> 16) : (int)(int16_t)(w[kk >> 1] & 0xFFFFu);
                 if (v != 0) {
                     if (run >= 16) atomicAdd(&h[0xF0], (uint32_t)(run >> 4));
                     atomicAdd(&h[((run & 15) << 4) | category_of(v)], 1u);
@@ -433,7 +460,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
                     ++run;
                 }
             }
-            if (run) atomicAdd(&h[0], 1u);  // EOB
+            if (half && run) atomicAdd(&h[0], 1u);  // EOB
         }
         __syncthreads();
         DMMT_TRACE(4);
