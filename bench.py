@@ -38,7 +38,9 @@ CONFIGS = {
     # name: (width, height, subsampling, quality, frames per step)
     "4k444q90": (3840, 2160, 0, 90, 1),
     "1080p420q75x256": (1920, 1080, 2, 75, 256),
+    "8k420q50": (7680, 4320, 2, 50, 1),   # BASELINE config 5 quality sweep (q50 = the Specification tables)
     "8k420q75": (7680, 4320, 2, 75, 1),
+    "8k420q95": (7680, 4320, 2, 95, 1),
 }
 
 

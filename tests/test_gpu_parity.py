@@ -178,6 +178,16 @@ def test_4k_quality90_444(encoder):
     assert gpu == oracle.encode(rgb, 255, 0, luma, chroma)
 
 
+@pytest.mark.parametrize("quality", [50, 95])
+def test_8k_quality_sweep_420(encoder, quality):
+    """BASELINE config 5 frame (7680x4320, 4:2:0) at the ends of the quality sweep;
+    q50 is the reference's Specification preset."""
+    luma, chroma = dmmt_jpeg.quality_tables(quality)
+    rgb = synthetic(7680, 4320, frame=quality)
+    gpu = encoder.encode(dmmt_jpeg.Image.from_array(rgb), opts(2, luma, chroma))
+    assert gpu == oracle.encode(rgb, 255, 2, luma, chroma, threads=8)
+
+
 def test_1080p_batch_quality75_420(encoder):
     """BASELINE config 3 shape (a few of the 256 frames; each byte-exact)."""
     luma, chroma = dmmt_jpeg.quality_tables(75)
