@@ -39,6 +39,7 @@ class RefOptions(ctypes.Structure):
         ("bits_per_channel", ctypes.c_int),
         ("luma_q", ctypes.c_uint8 * 64),
         ("chroma_q", ctypes.c_uint8 * 64),
+        ("restart_interval", ctypes.c_int),
     ]
 
 
@@ -92,10 +93,11 @@ class OracleError(RuntimeError):
         self.code = code
 
 
-def make_options(preset: int, luma_q, chroma_q, bits_per_channel: int = 8) -> RefOptions:
+def make_options(preset: int, luma_q, chroma_q, bits_per_channel: int = 8, restart_interval: int = 0) -> RefOptions:
     o = RefOptions()
     o.preset = int(preset)
     o.bits_per_channel = int(bits_per_channel)
+    o.restart_interval = int(restart_interval)
     for i in range(64):
         o.luma_q[i] = int(luma_q[i])
         o.chroma_q[i] = int(chroma_q[i])
@@ -109,11 +111,13 @@ def _as_u16_rgb(rgb) -> np.ndarray:
     return a
 
 
-def encode(rgb, maxval: int, preset: int, luma_q, chroma_q, bits_per_channel: int = 8, threads: int = 1) -> bytes:
-    """Whole reference encode path (JpegImageWriter::write_image, jpeg.rs:64-75)."""
+def encode(rgb, maxval: int, preset: int, luma_q, chroma_q, bits_per_channel: int = 8, threads: int = 1,
+           restart_interval: int = 0) -> bytes:
+    """Whole reference encode path (JpegImageWriter::write_image, jpeg.rs:64-75).
+    restart_interval > 0: the DRI/RSTn extension (not in the reference)."""
     a = _as_u16_rgb(rgb)
     h, w, _ = a.shape
-    opt = make_options(preset, luma_q, chroma_q, bits_per_channel)
+    opt = make_options(preset, luma_q, chroma_q, bits_per_channel, restart_interval)
     out = ctypes.c_void_p()
     n = ctypes.c_size_t()
     L = lib()
@@ -145,10 +149,10 @@ def forward(rgb, maxval: int, preset: int, luma_q, chroma_q) -> np.ndarray:
 
 
 def encode_coefficients(coef_zz: np.ndarray, width: int, height: int, preset: int, luma_q, chroma_q,
-                        bits_per_channel: int = 8) -> bytes:
+                        bits_per_channel: int = 8, restart_interval: int = 0) -> bytes:
     """Back half: emission-order zigzag blocks -> complete JPEG file."""
     c = np.ascontiguousarray(coef_zz, dtype=np.int16)
-    opt = make_options(preset, luma_q, chroma_q, bits_per_channel)
+    opt = make_options(preset, luma_q, chroma_q, bits_per_channel, restart_interval)
     out = ctypes.c_void_p()
     n = ctypes.c_size_t()
     L = lib()

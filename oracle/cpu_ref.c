@@ -393,9 +393,12 @@ int ref_encode_coefficients(const int16_t* coef_zz, size_t nblocks, int width, i
     memset(hist, 0, sizeof hist);
     int16_t* dcdiff = (int16_t*)malloc(sizeof(int16_t) * nblocks);
     if (!dcdiff) return REF_E_OOM;
+    const int ri = opt->restart_interval > 0 ? opt->restart_interval : 0;
     int last_dc[3] = {0, 0, 0};
     for (size_t e = 0; e < nblocks; ++e) {
         int k = (int)(e % (size_t)bpm);
+        if (ri && k == 0 && (e / (size_t)bpm) % (size_t)ri == 0) /* extension: predictors reset per interval */
+            last_dc[0] = last_dc[1] = last_dc[2] = 0;
         int comp = k < n_luma ? 0 : (k == n_luma ? 1 : 2);
         const int16_t* blk = coef_zz + e * 64;
         int16_t diff = (int16_t)(blk[0] - last_dc[comp]); /* i16 subtraction */
@@ -483,6 +486,10 @@ int ref_encode_coefficients(const int16_t* coef_zz, size_t nblocks, int width, i
     put_dht(&b, 0x00, sym[0], lens[0], nsym[0]);
     put_dht(&b, 0x13, sym[3], lens[3], nsym[3]);
     put_dht(&b, 0x02, sym[2], lens[2], nsym[2]);
+    if (ri) { /* extension: DRI (ITU T.81 B.2.4.4) */
+        uint8_t dri[2] = {(uint8_t)(ri >> 8), (uint8_t)ri};
+        put_segment(&b, 0xFF, 0xDD, dri, 2);
+    }
     { /* encoder.rs:247-262 */
         static const uint8_t sos[10] = {0x03, 0x01, 0x01, 0x02, 0x23, 0x03, 0x23, 0x00, 0x3F, 0x00};
         put_segment(&b, 0xFF, 0xDA, sos, 10);
@@ -495,6 +502,14 @@ int ref_encode_coefficients(const int16_t* coef_zz, size_t nblocks, int width, i
         int k = (int)(e % (size_t)bpm);
         int t = k < n_luma ? 0 : 2;
         const int16_t* blk = coef_zz + e * 64;
+        if (ri && k == 0 && e > 0 && (e / (size_t)bpm) % (size_t)ri == 0) {
+            /* extension: end of a restart interval -- 1-padding to a byte boundary
+             * (the pad byte stuffed like any other), then RSTm, m = interval index mod 8,
+             * which is not stuffed (ITU T.81 F.1.2.3) */
+            bw_flush(&w);
+            bb_put(&b, 0xFF);
+            bb_put(&b, (uint8_t)(0xD0 + ((e / (size_t)bpm / (size_t)ri - 1) & 7)));
+        }
         int diff = dcdiff[e];
         int cat = ref_category(diff);
         if (clen[t][cat] == 0) {

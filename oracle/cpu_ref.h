@@ -41,6 +41,7 @@ typedef struct {
     int bits_per_channel; /* written into SOF only (encoder.rs:235) */
     uint8_t luma_q[64];
     uint8_t chroma_q[64];
+    int restart_interval; /* extension (not in the reference): DRI + RSTn every N MCUs, 0 = reference */
 } ref_options;
 
 /* ---- stage entry points (each cites the reference function it restates) ---- */

@@ -126,6 +126,8 @@ class _BitReader:
                     i += 2
                     continue
                 if 0xD0 <= nb <= 0xD7:
+                    if nb - 0xD0 != len(self.segments) % 8:  # RSTm cycles 0..7 (T.81 F.1.2.3)
+                        raise ValueError("restart marker out of sequence")
                     self.segments.append(bytes(cur))
                     cur = bytearray()
                     i += 2
