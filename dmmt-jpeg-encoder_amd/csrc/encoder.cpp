@@ -50,8 +50,8 @@ struct dmmt_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grown on demand, never shrunk)
-    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_bits, total_ff, stage, chunk_bits, chunk_ff,
-        chunk_edge, chunk_bit0, chunk_ffpre, status, lut, qtab, qtab_u8;
+    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff, chunk_edge,
+        chunk_bit0, chunk_out, status, lut, qtab, qtab_u8;
     // host-API staging
     DevBuf in, out, out_len, dct;
     // uploaded table state
@@ -110,7 +110,7 @@ int validate(const dmmt_options* opt) {
     if (opt->bits_per_channel < 0 || opt->bits_per_channel > 255) return DMMT_E_INVALID_ARGUMENT;
     for (int i = 0; i < 64; ++i)
         if (opt->luma_q[i] == 0 || opt->chroma_q[i] == 0) return DMMT_E_INVALID_ARGUMENT;
-    if (opt->restart_interval != 0) return DMMT_E_INVALID_ARGUMENT;  // extension not enabled yet
+    if (opt->restart_interval < 0 || opt->restart_interval > 65535) return DMMT_E_INVALID_ARGUMENT;  // DRI is u16
     return DMMT_OK;
 }
 
@@ -171,15 +171,14 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     if ((rc = ensure(c->chunk_ff, nch * 8 * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(c->chunk_edge, nch * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(c->chunk_bit0, nch * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c->chunk_ffpre, nch * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(c->chunk_out, nch * sizeof(unsigned long long)))) return rc;
     // k_front / k_dcdiff add into the replicas, k_emit zeroes them after k_tables:
     // zero between launches, starting with the allocation
     if ((rc = ensure(c->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
     if ((rc = ensure(c->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
     if ((rc = ensure(c->code_tab, (size_t)nf * 1024 * 4))) return rc;
     if ((rc = ensure(c->hdr_len, (size_t)nf * 4))) return rc;
-    if ((rc = ensure(c->total_bits, (size_t)nf * 8))) return rc;
-    if ((rc = ensure(c->total_ff, (size_t)nf * 8))) return rc;
+    if ((rc = ensure(c->total_out, (size_t)nf * 8))) return rc;
     if ((rc = ensure(c->status, 16, true))) return rc;
     w->coef = (int16_t*)c->coef.p;
     w->dc = (int16_t*)c->dc.p;
@@ -188,14 +187,13 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     w->dc_hist = (uint32_t*)c->dc_hist.p;
     w->code_tab = (uint32_t*)c->code_tab.p;
     w->hdr_len = (uint32_t*)c->hdr_len.p;
-    w->total_bits = (unsigned long long*)c->total_bits.p;
     w->stage = (uint32_t*)c->stage.p;
     w->chunk_bits = (uint32_t*)c->chunk_bits.p;
     w->chunk_ff = (uint32_t*)c->chunk_ff.p;
     w->chunk_edge = (uint32_t*)c->chunk_edge.p;
     w->chunk_bit0 = (unsigned long long*)c->chunk_bit0.p;
-    w->chunk_ffpre = (uint32_t*)c->chunk_ffpre.p;
-    w->total_ff = (unsigned long long*)c->total_ff.p;
+    w->chunk_out = (unsigned long long*)c->chunk_out.p;
+    w->total_out = (unsigned long long*)c->total_out.p;
     w->status = (int*)c->status.p;
     w->norm_lut = nullptr;  // bound by prepare() after upload_tables
     w->qtab = nullptr;
@@ -413,8 +411,8 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     destroy_graphs(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
     DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff,     &c->ac_hist,     &c->dc_hist,
-                      &c->code_tab,   &c->hdr_len,    &c->total_bits, &c->total_ff,    &c->stage,
-                      &c->chunk_bits, &c->chunk_ff,   &c->chunk_edge, &c->chunk_bit0,  &c->chunk_ffpre,
+                      &c->code_tab,   &c->hdr_len,    &c->total_out,  &c->stage,
+                      &c->chunk_bits, &c->chunk_ff,   &c->chunk_edge, &c->chunk_bit0,  &c->chunk_out,
                       &c->status,     &c->lut,        &c->qtab,       &c->qtab_u8,     &c->in,
                       &c->out,        &c->out_len,    &c->dct};
     for (DevBuf* b : bufs) release(*b);

@@ -12,16 +12,22 @@
 //                of the 8 residues the chunk's start can have modulo 8, the 0xFF
 //                bytes lying wholly inside it -- so no later pass re-reads the
 //                stream to count them.
-//  k_offsets     one workgroup per frame: scan of the chunk bit counts (every
-//                chunk's bit offset); each chunk's 0xFF count at its actual
-//                alignment plus the byte it shares with the next chunk (built from
-//                the recorded edge bits); scan of those (every chunk's offset in
-//                the stuffed scan).
+//  k_offsets     one workgroup per frame: segmented scan of the chunk bit counts
+//                (every chunk's bit offset in its restart segment); each chunk's
+//                output bytes -- its bytes, a 0x00 per 0xFF (k_emit's count at its
+//                actual alignment plus the byte it shares with the next chunk,
+//                built from the recorded edge bits), the RST marker closing a
+//                segment -- and their scan (every chunk's place in the file).
 //  k_stuffwrite  one workgroup per chunk: the bytes whose first bit lies in the
 //                chunk, shifted out of its staging slot (the last one built from
 //                the edge bits, 1-padded at the end of the scan), a 0x00 after
 //                every 0xFF, staged in LDS and stored coalesced after the header;
-//                EOI and the file size by the frame's last chunk.
+//                RSTm after a segment's last chunk, EOI and the file size by the
+//                frame's last chunk.
+//
+// Restart intervals (extension, DRI/RSTn every N MCUs): each segment's scan
+// starts byte-aligned, so the chunk grid restarts with every segment and the
+// 1-padding closes each segment like the end of the scan.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -43,6 +49,28 @@ static_assert(kChunkBlocks == 256, "one thread per block, one workgroup per chun
 constexpr int kEmitWords = 4096;
 // Bytes per pass of k_stuffwrite (16 per thread).
 constexpr int kStuffPass = 4096;
+
+// Chunk c of a frame: blocks [el0, el0 + nb) of restart segment seg (the chunk
+// grid restarts with every segment; one segment without restart intervals).
+struct ChunkSpan {
+    long long el0;
+    int nb;
+    int seg;
+    bool seg_first, seg_last;
+};
+
+__device__ __forceinline__ ChunkSpan chunk_span(const Geom& g, int c) {
+    ChunkSpan r;
+    r.seg = min(c / g.cps, g.nseg - 1);
+    const int j = c - r.seg * g.cps;
+    const long long sb = (long long)r.seg * g.seg_blocks;
+    const long long se = min(sb + g.seg_blocks, g.bpf);
+    r.el0 = sb + (long long)j * kChunkBlocks;
+    r.nb = (int)min((long long)kChunkBlocks, se - r.el0);
+    r.seg_first = j == 0;
+    r.seg_last = r.el0 + r.nb == se;
+    return r;
+}
 
 // One thread walks one block (64 zigzag coefficients held in 32 registers) in
 // stream order (encoder.rs:356-404; categorize.rs:132-169): DC code + extra bits,
@@ -161,8 +189,9 @@ __global__ __launch_bounds__(256) void k_emit(const int16_t* coef, const int16_t
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
     const unsigned chunk = blockIdx.x;
-    const long long el0 = (long long)chunk * kChunkBlocks;
-    const int nb = (int)min((long long)kChunkBlocks, g.bpf - el0);
+    const ChunkSpan span = chunk_span(g, (int)chunk);
+    const long long el0 = span.el0;
+    const int nb = span.nb;
     const long long e = (long long)frame * g.bpf + el0 + tid;
     const size_t cid = (size_t)frame * g.nch + chunk;
     for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
@@ -263,8 +292,8 @@ __global__ __launch_bounds__(256) void k_emit(const int16_t* coef, const int16_t
 }
 
 // The byte that starts m1 (1..7) bits before the end of a chunk: those last m1
-// bits of the chunk, then the next chunk's first bits, then 1-bits where the scan
-// ends (binary_stream.rs:89-96).
+// bits of the chunk, then the next chunk's first bits (same restart segment),
+// then 1-bits where the segment or the scan ends (binary_stream.rs:89-96).
 __device__ __forceinline__ uint32_t boundary_byte(int m1, uint32_t last16, bool has_next, uint32_t n_next,
                                                   uint32_t first16_next) {
     uint32_t v = last16 & ((1u << m1) - 1u);
@@ -277,21 +306,28 @@ __device__ __forceinline__ uint32_t boundary_byte(int m1, uint32_t last16, bool 
     return ((v << m2) | ((1u << m2) - 1u)) & 0xFFu;
 }
 
-// 0xFF bytes whose first bit lies in chunk c (starting at scan bit b0): the
-// interior ones at the chunk's alignment + the byte it shares with the next chunk.
-__device__ __forceinline__ uint32_t chunk_ff_count(const uint32_t* __restrict__ cff, const uint32_t* __restrict__ cbits,
-                                                   const uint32_t* __restrict__ cedge, int nch, int c,
-                                                   unsigned long long b0) {
+// Output bytes of chunk c, whose bits start at b0 inside its (byte-aligned)
+// restart segment: the bytes whose first bit lies in the chunk, a 0x00 after each
+// of them that is 0xFF (the interior ones counted by k_emit at the chunk's
+// alignment, plus the byte it shares with the next chunk or the 1-padding), and
+// the RST marker after the last chunk of every segment but the frame's last.
+__device__ __forceinline__ unsigned long long chunk_out_bytes(const uint32_t* __restrict__ cff,
+                                                              const uint32_t* __restrict__ cbits,
+                                                              const uint32_t* __restrict__ cedge, const Geom& g,
+                                                              int c, unsigned long long b0) {
+    const ChunkSpan sp = chunk_span(g, c);
     const uint32_t n = cbits[c];
     const unsigned long long e = b0 + n;
-    uint32_t ffc = cff[(size_t)c * 8 + ((8 - (b0 & 7)) & 7)];
+    unsigned long long out = ((e + 7) >> 3) - ((b0 + 7) >> 3);
+    out += cff[(size_t)c * 8 + ((8 - (b0 & 7)) & 7)];
     if ((e & 7) && (e & ~7ull) >= b0) {
-        const bool has_next = c + 1 < nch;
+        const bool has_next = !sp.seg_last;
         const uint32_t byte = boundary_byte((int)(e & 7), cedge[c] & 0xFFFFu, has_next, has_next ? cbits[c + 1] : 0u,
                                             has_next ? cedge[c + 1] >> 16 : 0u);
-        ffc += byte == 0xFFu ? 1u : 0u;
+        out += byte == 0xFFu ? 1u : 0u;
     }
-    return ffc;
+    if (sp.seg_last && c != g.nch - 1) out += 2;  // RSTm (extension)
+    return out;
 }
 
 // workgroup (1024 threads) exclusive scan; *tot receives the total
@@ -311,15 +347,62 @@ __device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long
     return pre;
 }
 
+// Segmented (flag, value) pair: value accumulated since the last segment start.
+// (f1, v1) + (f2, v2) = (f1 | f2, f2 ? v2 : v1 + v2), associative.
+__device__ __forceinline__ void seg_combine(bool& f, unsigned long long& v, bool f2, unsigned long long v2) {
+    v = f2 ? v2 : v + v2;
+    f = f || f2;
+}
+
+// workgroup (1024 threads) exclusive segmented scan of (flag, value)
+__device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigned long long v,
+                                                                 unsigned long long* sWaveV, int* sWaveF) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    bool fi = f;
+    unsigned long long vi = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // inclusive within the wave
+        const unsigned long long pv = __shfl_up(vi, d, 64);
+        const int pf = __shfl_up((int)fi, d, 64);
+        if (lane >= d) {
+            bool ff = pf != 0;
+            unsigned long long vv = pv;
+            seg_combine(ff, vv, fi, vi);
+            fi = ff;
+            vi = vv;
+        }
+    }
+    if (lane == 63) {
+        sWaveV[wave] = vi;
+        sWaveF[wave] = fi;
+    }
+    // exclusive within the wave
+    unsigned long long ve = __shfl_up(vi, 1, 64);
+    int fe = __shfl_up((int)fi, 1, 64);
+    if (lane == 0) {
+        ve = 0;
+        fe = 0;
+    }
+    __syncthreads();
+    bool cf = false;
+    unsigned long long cv = 0;
+    for (int q = 0; q < wave; ++q) seg_combine(cf, cv, sWaveF[q] != 0, sWaveV[q]);
+    bool rf = cf;
+    unsigned long long rv = cv;
+    seg_combine(rf, rv, fe != 0, ve);
+    __syncthreads();
+    return rv;
+}
+
 // -------------------------------------------------------------------- k_offsets
 __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ chunk_bits,
                                                   const uint32_t* __restrict__ chunk_ff,
                                                   const uint32_t* __restrict__ chunk_edge, Geom g,
                                                   unsigned long long* __restrict__ chunk_bit0,
-                                                  uint32_t* __restrict__ chunk_ffpre,
-                                                  unsigned long long* __restrict__ total_bits,
-                                                  unsigned long long* __restrict__ total_ff) {
+                                                  unsigned long long* __restrict__ chunk_out,
+                                                  unsigned long long* __restrict__ total_out) {
     __shared__ unsigned long long sWave[16];
+    __shared__ int sWaveF[16];
     const int tid = threadIdx.x;
     const int frame = blockIdx.x;
     const int nch = g.nch;
@@ -327,30 +410,30 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
     const uint32_t* cff = chunk_ff + (size_t)frame * nch * 8;
     const uint32_t* cedge = chunk_edge + (size_t)frame * nch;
     unsigned long long* bit0 = chunk_bit0 + (size_t)frame * nch;
-    uint32_t* ffpre = chunk_ffpre + (size_t)frame * nch;
+    unsigned long long* outo = chunk_out + (size_t)frame * nch;
     const int per = (nch + 1023) / 1024;
     const int c0 = min(tid * per, nch), c1 = min(c0 + per, nch);
 
-    unsigned long long mine = 0, tb = 0, tf = 0;
-    for (int c = c0; c < c1; ++c) mine += cbits[c];
-    const unsigned long long run0 = block_scan_1024(mine, sWave, &tb);
-    unsigned long long run = run0, ffsum = 0;
+    // bit offsets inside the restart segments: segmented scan of the chunk bits
+    bool f = false;
+    unsigned long long v = 0;
+    for (int c = c0; c < c1; ++c) seg_combine(f, v, chunk_span(g, c).seg_first, cbits[c]);
+    unsigned long long run = block_segscan_1024(f, v, sWave, sWaveF);
+    unsigned long long mine = 0;
     for (int c = c0; c < c1; ++c) {
+        if (chunk_span(g, c).seg_first) run = 0;
         bit0[c] = run;
-        ffsum += chunk_ff_count(cff, cbits, cedge, nch, c, run);
+        mine += chunk_out_bytes(cff, cbits, cedge, g, c, run);
         run += cbits[c];
     }
-    unsigned long long frun = block_scan_1024(ffsum, sWave, &tf);
-    run = run0;
+    // output offsets: plain scan of the chunk output bytes
+    unsigned long long tot = 0;
+    unsigned long long orun = block_scan_1024(mine, sWave, &tot);
     for (int c = c0; c < c1; ++c) {
-        ffpre[c] = (uint32_t)frun;
-        frun += chunk_ff_count(cff, cbits, cedge, nch, c, run);
-        run += cbits[c];
+        outo[c] = orun;
+        orun += chunk_out_bytes(cff, cbits, cedge, g, c, bit0[c]);
     }
-    if (tid == 0) {
-        total_bits[frame] = tb;
-        total_ff[frame] = tf;
-    }
+    if (tid == 0) total_out[frame] = tot;
 }
 
 // ----------------------------------------------------------------- k_stuffwrite
@@ -358,9 +441,8 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ chunk_bits,
                                                     const uint32_t* __restrict__ chunk_edge,
                                                     const unsigned long long* __restrict__ chunk_bit0,
-                                                    const uint32_t* __restrict__ chunk_ffpre,
-                                                    const unsigned long long* __restrict__ total_bits,
-                                                    const unsigned long long* __restrict__ total_ff,
+                                                    const unsigned long long* __restrict__ chunk_out,
+                                                    const unsigned long long* __restrict__ total_out,
                                                     const uint32_t* __restrict__ hdr_len, Geom g,
                                                     uint8_t* __restrict__ out, size_t out_stride,
                                                     uint32_t* __restrict__ out_len, int* __restrict__ status) {
@@ -371,8 +453,7 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
     const int c = blockIdx.x;
     const size_t cid = (size_t)frame * g.nch + c;
     const uint32_t hdr = hdr_len[frame];
-    const unsigned long long scan_bytes = (total_bits[frame] + 7) >> 3;
-    const unsigned long long end = (unsigned long long)hdr + scan_bytes + total_ff[frame];
+    const unsigned long long end = (unsigned long long)hdr + total_out[frame];
     if (end + 2 > out_stride) {  // uniform over the frame
         if (c == 0 && tid == 0) {
             out_len[frame] = 0;  // reported as DMMT_E_CAPACITY by the host
@@ -380,12 +461,19 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
         }
         return;
     }
+    const ChunkSpan sp = chunk_span(g, c);
     const bool last = c == g.nch - 1;
-    if (last && tid == 0) {  // EOI (encoder.rs:131) and the file size
-        uint8_t* of = out + (size_t)frame * out_stride;
-        of[end] = 0xFF;
-        of[end + 1] = 0xD9;
-        out_len[frame] = (uint32_t)(end + 2);
+    uint8_t* const base = out + (size_t)frame * out_stride + hdr;
+    if (tid == 0) {
+        if (last) {  // EOI (encoder.rs:131) and the file size
+            base[total_out[frame]] = 0xFF;
+            base[total_out[frame] + 1] = 0xD9;
+            out_len[frame] = (uint32_t)(end + 2);
+        } else if (sp.seg_last) {  // RSTm closing restart segment m (extension; not stuffed)
+            const unsigned long long at = chunk_out[cid + 1] - 2;
+            base[at] = 0xFF;
+            base[at + 1] = (uint8_t)(0xD0 + (sp.seg & 7));
+        }
     }
     const unsigned long long b0 = chunk_bit0[cid];
     const uint32_t n = chunk_bits[cid];
@@ -397,13 +485,13 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
     const bool shared_tail = (e & 7) != 0;
     uint32_t tail = 0;
     if (shared_tail) {
-        const bool has_next = !last;
+        const bool has_next = !sp.seg_last;
         tail = boundary_byte((int)(e & 7), chunk_edge[cid] & 0xFFFFu, has_next, has_next ? chunk_bits[cid + 1] : 0u,
                              has_next ? chunk_edge[cid + 1] >> 16 : 0u);
     }
     const uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
     const unsigned off = (unsigned)(8 * kbeg - b0);  // the first owned byte starts this many bits into the chunk
-    uint8_t* o = out + (size_t)frame * out_stride + hdr + kbeg + chunk_ffpre[cid];
+    uint8_t* o = base + chunk_out[cid];
     for (unsigned long long pos = 0; pos < nbytes; pos += kStuffPass) {  // uniform
         const unsigned long long kb = pos + 16u * (unsigned)tid;          // first of my 16 bytes (chunk-relative)
         uint8_t v[16];
@@ -464,8 +552,8 @@ hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t s
 
 hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
     hipLaunchKernelGGL(k_offsets, dim3(n_frames), dim3(1024), 0, st, (const uint32_t*)w.chunk_bits,
-                       (const uint32_t*)w.chunk_ff, (const uint32_t*)w.chunk_edge, g, w.chunk_bit0, w.chunk_ffpre,
-                       w.total_bits, w.total_ff);
+                       (const uint32_t*)w.chunk_ff, (const uint32_t*)w.chunk_edge, g, w.chunk_bit0, w.chunk_out,
+                       w.total_out);
     return hipGetLastError();
 }
 
@@ -473,9 +561,9 @@ hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t
                              uint32_t* out_len, hipStream_t st) {
     hipLaunchKernelGGL(k_stuffwrite, dim3(g.nch, n_frames), dim3(256), 0, st, (const uint32_t*)w.stage,
                        (const uint32_t*)w.chunk_bits, (const uint32_t*)w.chunk_edge,
-                       (const unsigned long long*)w.chunk_bit0, (const uint32_t*)w.chunk_ffpre,
-                       (const unsigned long long*)w.total_bits, (const unsigned long long*)w.total_ff,
-                       (const uint32_t*)w.hdr_len, g, out, out_stride, out_len, w.status);
+                       (const unsigned long long*)w.chunk_bit0, (const unsigned long long*)w.chunk_out,
+                       (const unsigned long long*)w.total_out, (const uint32_t*)w.hdr_len, g, out, out_stride,
+                       out_len, w.status);
     return hipGetLastError();
 }
 

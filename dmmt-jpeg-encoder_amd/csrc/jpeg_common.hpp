@@ -34,7 +34,10 @@ struct Geom {
     int maxval;             // PPM max value
     int restart_interval;   // 0 = reference behaviour
     long long bpf;          // blocks per frame
-    int nch;                // entropy chunks per frame
+    int nch;                // entropy chunks per frame (chunks never straddle a restart segment)
+    int nseg;               // restart segments per frame (1 without restart intervals)
+    int cps;                // chunks per full segment
+    long long seg_blocks;   // blocks per full segment
     long long max_scan_bytes;  // worst-case entropy-coded bytes per frame (before stuffing)
 };
 
@@ -54,14 +57,21 @@ inline Geom make_geom(int width, int height, int subsampling, int maxval, int re
     g.maxval = maxval;
     g.restart_interval = restart_interval;
     g.bpf = (long long)g.nmcu * g.bpm;
-    g.nch = (int)((g.bpf + kChunkBlocks - 1) / kChunkBlocks);
+    // restart segments (extension): every restart_interval MCUs the scan restarts
+    // byte-aligned; the chunk grid restarts with it
+    g.nseg = restart_interval > 0 ? (g.nmcu + restart_interval - 1) / restart_interval : 1;
+    g.seg_blocks = restart_interval > 0 ? (long long)restart_interval * g.bpm : g.bpf;
+    g.cps = (int)((g.seg_blocks + kChunkBlocks - 1) / kChunkBlocks);
+    const long long last_seg_blocks = g.bpf - (long long)(g.nseg - 1) * g.seg_blocks;
+    g.nch = (g.nseg - 1) * g.cps + (int)((last_seg_blocks + kChunkBlocks - 1) / kChunkBlocks);
     g.max_scan_bytes = (g.bpf * kMaxBlockBits + 7) / 8;
     return g;
 }
 
-// Worst-case JPEG size: header + every scan byte stuffed + RST markers + EOI.
+// Worst-case JPEG size: header + every scan byte stuffed + per restart segment a
+// stuffed pad byte and the RST marker + EOI.
 inline size_t max_jpeg_bytes(const Geom& g) {
-    return (size_t)kMaxHeaderBytes + (size_t)g.max_scan_bytes * 2 + 2 * (size_t)g.nmcu + 2 + 64;
+    return (size_t)kMaxHeaderBytes + (size_t)g.max_scan_bytes * 2 + 4 * (size_t)g.nmcu + 2 + 64;
 }
 
 }  // namespace dmmt

@@ -16,14 +16,13 @@ struct Work {
     uint32_t* dc_hist;              // [frames][reps][2][16], zero between launches
     uint32_t* code_tab;             // [frames][4][256]  (len << 16) | code
     uint32_t* hdr_len;              // [frames]
-    unsigned long long* total_bits; // [frames]
     uint32_t* stage;                // [frames][nch][kChunkWordsCap] each chunk's own bit stream, MSB first
     uint32_t* chunk_bits;           // [frames][nch] bits of the chunk
     uint32_t* chunk_ff;             // [frames][nch][8] 0xFF bytes inside the chunk per alignment residue
     uint32_t* chunk_edge;           // [frames][nch] first 16 bits << 16 | last 16 bits
-    unsigned long long* chunk_bit0; // [frames][nch] bit offset of the chunk in the scan
-    uint32_t* chunk_ffpre;          // [frames][nch] 0xFF bytes in the scan before the chunk's bytes
-    unsigned long long* total_ff;   // [frames] 0xFF bytes of the scan
+    unsigned long long* chunk_bit0; // [frames][nch] bit offset of the chunk in its restart segment
+    unsigned long long* chunk_out;  // [frames][nch] offset of the chunk's output bytes after the header
+    unsigned long long* total_out;  // [frames] stuffed scan bytes incl. RST markers
     int* status;                    // error bits: 1 value>max, 2 table, 16 output capacity
     const float* norm_lut;          // maxval-normalisation table
     const float* qtab;              // [2][64] f32
