@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -69,6 +70,11 @@ struct dmmt_ctx {
     bool use_graphs = false;
     std::vector<GraphEntry> graphs;
     uint64_t graph_clock = 0;
+    // MCU-row stripe between dmmt_stripe_analyze and dmmt_stripe_encode
+    bool stripe_pending = false;
+    Geom stripe_g{};
+    dmmt_options stripe_opt{};
+    int stripe_sb = 1;
 };
 
 namespace {
@@ -264,8 +270,8 @@ struct StageTimer {
 // k_stuffwrite) for coefficients already in w.coef / w.dc with AC histograms
 // accumulated.
 int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bits, uint8_t* out, size_t out_stride,
-                      uint32_t* out_len, hipStream_t st) {
-    {
+                      uint32_t* out_len, hipStream_t st, bool dc_done = false) {
+    if (!dc_done) {  // (a stripe's DC differences and counts come from dmmt_stripe_analyze)
         StageTimer t(c, ST_DCDIFF, st);
         HIP_TRY(launch_dcdiff(nf, g, w, st));
     }
@@ -759,8 +765,140 @@ extern "C" int dmmt_fill_synthetic(dmmt_ctx* c, void* d_rgb, uint16_t width, uin
     if (!c || !d_rgb || n_frames <= 0) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = set_device(c))) return rc;
-    HIP_TRY(launch_synthetic((uint8_t*)d_rgb, width, height, n_frames, first_frame, seed, c->stream));
+    HIP_TRY(launch_synthetic((uint8_t*)d_rgb, width, height, n_frames, first_frame, seed, 0, height, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_fill_synthetic_rows(dmmt_ctx* c, void* d_rgb, uint16_t width, uint16_t height, int32_t row0,
+                                        int32_t rows, int32_t frame, uint32_t seed) {
+    if (!c || !d_rgb || row0 < 0 || rows <= 0 || row0 + rows > height) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    HIP_TRY(launch_synthetic((uint8_t*)d_rgb, width, height, 1, frame, seed, row0, rows, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DMMT_OK;
+}
+
+// ---------------------------------------------------------------- stripes
+// One image across several GPUs (extension): each context encodes a run of
+// whole MCU rows that starts (and, unless it ends the image, ends) on a restart
+// interval boundary.  The Huffman tables are global per image, so the only
+// exchange is the element-wise sum of the stripes' symbol histograms between the
+// two calls; the stripes' outputs then concatenate to exactly the single-GPU
+// encode with the same restart interval.
+static int stripe_geom(const dmmt_stripe* st, const dmmt_options* opt, Geom* g) {
+    if (!st || !opt || !st->d_rgb) return DMMT_E_INVALID_ARGUMENT;
+    if (st->sample_bytes != 1 && st->sample_bytes != 2 && st->sample_bytes != 4) return DMMT_E_INVALID_ARGUMENT;
+    const int ri = opt->restart_interval;
+    if (ri <= 0) return DMMT_E_INVALID_ARGUMENT;  // stripes are restart segments
+    Geom full;
+    int rc;
+    if ((rc = make_checked_geom(st->width, st->height, opt->subsampling, st->maxval, ri, &full))) return rc;
+    if (st->mcu_row0 < 0 || st->mcu_rows <= 0 || st->mcu_row0 + st->mcu_rows > full.mcuy) return DMMT_E_INVALID_ARGUMENT;
+    const long long m0 = (long long)st->mcu_row0 * full.mcux;
+    const bool last = st->mcu_row0 + st->mcu_rows == full.mcuy;
+    if (m0 % ri) return DMMT_E_INVALID_ARGUMENT;  // must start a restart interval
+    if (!last && ((long long)st->mcu_rows * full.mcux) % ri) return DMMT_E_INVALID_ARGUMENT;  // and end one
+    const int rows_px = 8 * full.vr;
+    const int y0 = st->mcu_row0 * rows_px;
+    const int h = std::min(st->mcu_rows * rows_px, (int)st->height - y0);
+    *g = make_geom(st->width, h, opt->subsampling, st->maxval, ri);
+    g->sof_height = st->height;
+    g->seg_base = (int)(m0 / ri);
+    g->stripe_first = st->mcu_row0 == 0;
+    g->more_after = !last;
+    return DMMT_OK;
+}
+
+extern "C" size_t dmmt_stripe_max_bytes(const dmmt_stripe* st, const dmmt_options* opt) {
+    Geom g;
+    if (validate(opt) || stripe_geom(st, opt, &g)) return 0;
+    return max_jpeg_bytes(g);
+}
+
+extern "C" int dmmt_stripe_analyze(dmmt_ctx* c, const dmmt_stripe* st, const dmmt_options* opt,
+                                   uint64_t hist[DMMT_STRIPE_HIST_WORDS]) {
+    if (!c || !hist) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    Geom g;
+    if ((rc = validate(opt)) || (rc = stripe_geom(st, opt, &g))) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    hipStream_t s = c->stream;
+    Work w;
+    if ((rc = prepare(c, g, 1, opt, st->sample_bytes, s, &w))) return rc;
+    {
+        StageTimer t(c, ST_FRONT, s);
+        HIP_TRY(launch_front(st->d_rgb, (size_t)st->width * g.height * 3 * st->sample_bytes, st->sample_bytes, 1, g, w,
+                             s));
+    }
+    {
+        StageTimer t(c, ST_DCDIFF, s);
+        HIP_TRY(launch_dcdiff(1, g, w, s));
+    }
+    std::vector<uint32_t> ac((size_t)kHistReps * 512), dc((size_t)kHistReps * 32);
+    HIP_TRY(hipMemcpyAsync(ac.data(), w.ac_hist, ac.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(dc.data(), w.dc_hist, dc.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemsetAsync(w.ac_hist, 0, ac.size() * 4, s));  // consumed here; k_emit won't run before the encode
+    HIP_TRY(hipMemsetAsync(w.dc_hist, 0, dc.size() * 4, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if ((rc = take_status(c, s))) return rc;
+    // [luma DC 16][luma AC 256][chroma DC 16][chroma AC 256]
+    for (int i = 0; i < DMMT_STRIPE_HIST_WORDS; ++i) hist[i] = 0;
+    for (int r = 0; r < kHistReps; ++r) {
+        for (int k = 0; k < 16; ++k) {
+            hist[k] += dc[(size_t)r * 32 + k];
+            hist[272 + k] += dc[(size_t)r * 32 + 16 + k];
+        }
+        for (int k = 0; k < 256; ++k) {
+            hist[16 + k] += ac[(size_t)r * 512 + k];
+            hist[288 + k] += ac[(size_t)r * 512 + 256 + k];
+        }
+    }
+    c->stripe_g = g;
+    c->stripe_opt = *opt;
+    c->stripe_sb = st->sample_bytes;
+    c->stripe_pending = true;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_stripe_encode(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS], uint8_t* d_out,
+                                  size_t out_cap, uint64_t* out_len) {
+    if (!c || !hist_sum || !d_out || !out_len) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stripe_pending) return DMMT_E_INVALID_ARGUMENT;  // dmmt_stripe_analyze first
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const Geom g = c->stripe_g;
+    if (out_cap < max_jpeg_bytes(g)) return DMMT_E_CAPACITY;
+    hipStream_t s = c->stream;
+    Work w;
+    if ((rc = prepare(c, g, 1, &c->stripe_opt, c->stripe_sb, s, &w))) return rc;
+    // the summed histograms go into replica 0 (the other replicas are zero)
+    std::vector<uint32_t> ac(512), dc(32);
+    for (int k = 0; k < 16; ++k) {
+        if (hist_sum[k] > 0xFFFFFFFFull || hist_sum[272 + k] > 0xFFFFFFFFull) return DMMT_E_INVALID_ARGUMENT;
+        dc[k] = (uint32_t)hist_sum[k];
+        dc[16 + k] = (uint32_t)hist_sum[272 + k];
+    }
+    for (int k = 0; k < 256; ++k) {
+        if (hist_sum[16 + k] > 0xFFFFFFFFull || hist_sum[288 + k] > 0xFFFFFFFFull) return DMMT_E_INVALID_ARGUMENT;
+        ac[k] = (uint32_t)hist_sum[16 + k];
+        ac[256 + k] = (uint32_t)hist_sum[288 + k];
+    }
+    HIP_TRY(hipMemcpyAsync(w.ac_hist, ac.data(), ac.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(w.dc_hist, dc.data(), dc.size() * 4, hipMemcpyHostToDevice, s));
+    if ((rc = ensure(c->out_len, 4))) return rc;
+    if ((rc = enqueue_back_half(c, g, 1, w, c->stripe_opt.bits_per_channel, d_out, out_cap, (uint32_t*)c->out_len.p,
+                                s, true)))
+        return rc;
+    uint32_t len = 0;
+    HIP_TRY(hipMemcpyAsync(&len, c->out_len.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->stripe_pending = false;
+    if ((rc = take_status(c, s))) return rc;
+    *out_len = len;
     return DMMT_OK;
 }
 

@@ -326,7 +326,7 @@ __device__ __forceinline__ unsigned long long chunk_out_bytes(const uint32_t* __
                                             has_next ? cedge[c + 1] >> 16 : 0u);
         out += byte == 0xFFu ? 1u : 0u;
     }
-    if (sp.seg_last && c != g.nch - 1) out += 2;  // RSTm (extension)
+    if (sp.seg_last && (c != g.nch - 1 || g.more_after)) out += 2;  // RSTm (extension)
     return out;
 }
 
@@ -465,14 +465,15 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
     const bool last = c == g.nch - 1;
     uint8_t* const base = out + (size_t)frame * out_stride + hdr;
     if (tid == 0) {
-        if (last) {  // EOI (encoder.rs:131) and the file size
+        if (last && !g.more_after) {  // EOI (encoder.rs:131) and the file size
             base[total_out[frame]] = 0xFF;
             base[total_out[frame] + 1] = 0xD9;
             out_len[frame] = (uint32_t)(end + 2);
         } else if (sp.seg_last) {  // RSTm closing restart segment m (extension; not stuffed)
-            const unsigned long long at = chunk_out[cid + 1] - 2;
+            const unsigned long long at = (last ? total_out[frame] : chunk_out[cid + 1]) - 2;
             base[at] = 0xFF;
-            base[at + 1] = (uint8_t)(0xD0 + (sp.seg & 7));
+            base[at + 1] = (uint8_t)(0xD0 + ((g.seg_base + sp.seg) & 7));
+            if (last) out_len[frame] = (uint32_t)end;  // a stripe that more stripes follow
         }
     }
     const unsigned long long b0 = chunk_bit0[cid];

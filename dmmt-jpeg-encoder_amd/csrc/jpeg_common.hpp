@@ -39,6 +39,11 @@ struct Geom {
     int cps;                // chunks per full segment
     long long seg_blocks;   // blocks per full segment
     long long max_scan_bytes;  // worst-case entropy-coded bytes per frame (before stuffing)
+    // MCU-row stripe of a larger image (dmmt_stripe_*; a whole frame otherwise)
+    int sof_height;         // image height written into SOF
+    int seg_base;           // global index of the first restart segment (RSTm numbering)
+    int stripe_first;       // the stripe starts the image: write the header
+    int more_after;         // more stripes follow: close with RSTm instead of EOI
 };
 
 inline Geom make_geom(int width, int height, int subsampling, int maxval, int restart_interval) {
@@ -65,6 +70,10 @@ inline Geom make_geom(int width, int height, int subsampling, int maxval, int re
     const long long last_seg_blocks = g.bpf - (long long)(g.nseg - 1) * g.seg_blocks;
     g.nch = (g.nseg - 1) * g.cps + (int)((last_seg_blocks + kChunkBlocks - 1) / kChunkBlocks);
     g.max_scan_bytes = (g.bpf * kMaxBlockBits + 7) / 8;
+    g.sof_height = height;
+    g.seg_base = 0;
+    g.stripe_first = 1;
+    g.more_after = 0;
     return g;
 }
 

@@ -756,6 +756,10 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
 
     // ---- 6: header
     if (!sym_thread) return;
+    if (!g.stripe_first) {  // a later stripe of an image: tables only, no header
+        if (tab == 0 && s == 0) hdr_len[frame] = 0;
+        return;
+    }
     uint8_t* o = out + (size_t)frame * out_stride;
     const int pos_dht0 = 2 + 18 + 69 + 69 + 19;
     const int off_lac = pos_dht0;
@@ -793,7 +797,7 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
             sof[1] = 0xC0;
             put_be16(sof + 2, 17);
             sof[4] = (uint8_t)bits_per_channel;
-            put_be16(sof + 5, g.height);
+            put_be16(sof + 5, g.sof_height);
             put_be16(sof + 7, g.width);
             sof[9] = 3;
             sof[10] = 1;
@@ -872,12 +876,13 @@ __device__ __forceinline__ uint32_t xorshift32(uint32_t x) {
 }
 
 __global__ __launch_bounds__(256) void k_synthetic(uint8_t* __restrict__ rgb, int w, int h, int n_frames,
-                                                   int first_frame, uint32_t seed) {
-    const long long npx = (long long)w * h;
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < npx * n_frames;
+                                                   int first_frame, uint32_t seed, int row0, int rows) {
+    const long long npx = (long long)w * h;       // the whole frame (the noise index)
+    const long long nout = (long long)w * rows;   // rows [row0, row0 + rows) are generated
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nout * n_frames;
          i += (long long)gridDim.x * 256) {
-        const int fl = (int)(i / npx);
-        const long long pi = i - (long long)fl * npx;
+        const int fl = (int)(i / nout);
+        const long long pi = i - (long long)fl * nout + (long long)row0 * w;
         const int y = (int)(pi / w), x = (int)(pi - (long long)y * w);
         const uint32_t f = (uint32_t)(first_frame + fl);
         const uint32_t base = (uint32_t)(x + 8 * y) & 255u;
@@ -1016,11 +1021,11 @@ hipError_t launch_dct_blocks(float* data, long long nblocks, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_frame, uint32_t seed,
-                            hipStream_t st) {
-    const long long n = (long long)w * h * n_frames;
+hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_frame, uint32_t seed, int row0,
+                            int rows, hipStream_t st) {
+    const long long n = (long long)w * rows * n_frames;
     hipLaunchKernelGGL(k_synthetic, dim3(clampi((n + 255) / 256, 1, 8192)), dim3(256), 0, st, rgb, w, h, n_frames,
-                       first_frame, seed);
+                       first_frame, seed, row0, rows);
     return hipGetLastError();
 }
 

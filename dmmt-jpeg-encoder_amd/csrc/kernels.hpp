@@ -42,6 +42,7 @@ hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_
 hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
                              uint32_t* out_len, hipStream_t st);
 hipError_t launch_dct_blocks(float* data, long long nblocks, hipStream_t st);
-hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_frame, uint32_t seed, hipStream_t st);
+hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_frame, uint32_t seed, int row0,
+                            int rows, hipStream_t st);
 
 }  // namespace dmmt

@@ -105,6 +105,12 @@ def lib():
     L.dmmt_memcpy_h2d.argtypes = [vp, vp, vp, sz]
     L.dmmt_memcpy_d2h.argtypes = [vp, vp, vp, sz]
     L.dmmt_fill_synthetic.argtypes = [vp, vp, u16, u16, i32, i32, ctypes.c_uint32]
+    L.dmmt_fill_synthetic_rows.argtypes = [vp, vp, u16, u16, i32, i32, i32, ctypes.c_uint32]
+    H = ctypes.c_uint64 * STRIPE_HIST_WORDS
+    L.dmmt_stripe_analyze.argtypes = [vp, P(DmmtStripe), P(DmmtOptions), H]
+    L.dmmt_stripe_encode.argtypes = [vp, H, vp, sz, P(ctypes.c_uint64)]
+    L.dmmt_stripe_max_bytes.argtypes = [P(DmmtStripe), P(DmmtOptions)]
+    L.dmmt_stripe_max_bytes.restype = sz
     L.dmmt_build_info.argtypes = []
     L.dmmt_build_info.restype = ctypes.c_char_p
     _lib = L
@@ -129,6 +135,15 @@ class DmmtDeviceFrames(ctypes.Structure):
                 ("width", ctypes.c_uint16), ("height", ctypes.c_uint16), ("maxval", ctypes.c_uint16),
                 ("sample_bytes", ctypes.c_uint16), ("d_out", ctypes.c_void_p), ("out_stride", ctypes.c_size_t),
                 ("d_out_len", ctypes.c_void_p)]
+
+
+class DmmtStripe(ctypes.Structure):
+    _fields_ = [("d_rgb", ctypes.c_void_p), ("width", ctypes.c_uint16), ("height", ctypes.c_uint16),
+                ("maxval", ctypes.c_uint16), ("sample_bytes", ctypes.c_uint16), ("mcu_row0", ctypes.c_int32),
+                ("mcu_rows", ctypes.c_int32)]
+
+
+STRIPE_HIST_WORDS = 2 * (16 + 256)
 
 
 def _check(rc: int, what: str = ""):
@@ -392,6 +407,34 @@ class Encoder:
                        seed: int = 0x9E3779B9):
         _check(lib().dmmt_fill_synthetic(self._ctx, d_rgb, width, height, n_frames, first_frame, seed), "synthetic")
 
+    def fill_synthetic_rows(self, d_rgb: int, width: int, height: int, row0: int, rows: int, frame: int = 0,
+                            seed: int = 0x9E3779B9):
+        _check(lib().dmmt_fill_synthetic_rows(self._ctx, d_rgb, width, height, row0, rows, frame, seed), "synthetic")
+
+    # ---- one image over several GPUs (extension; include/dmmt_jpeg.h "dmmt_stripe")
+    @staticmethod
+    def stripe(d_rgb: int, width: int, height: int, mcu_row0: int, mcu_rows: int, maxval: int = 255,
+               sample_bytes: int = 1) -> DmmtStripe:
+        return DmmtStripe(d_rgb, width, height, maxval, sample_bytes, mcu_row0, mcu_rows)
+
+    @staticmethod
+    def stripe_max_bytes(stripe: DmmtStripe, options: JpegTransformationOptions) -> int:
+        return lib().dmmt_stripe_max_bytes(ctypes.byref(stripe), ctypes.byref(options.to_c()))
+
+    def stripe_analyze(self, stripe: DmmtStripe, options: JpegTransformationOptions) -> np.ndarray:
+        """front half of the stripe; returns its symbol histograms (uint64[544])"""
+        h = (ctypes.c_uint64 * STRIPE_HIST_WORDS)()
+        _check(lib().dmmt_stripe_analyze(self._ctx, ctypes.byref(stripe), ctypes.byref(options.to_c()), h),
+               "stripe_analyze")
+        return np.ctypeslib.as_array(h).copy()
+
+    def stripe_encode(self, hist_sum, d_out: int, out_cap: int) -> int:
+        """tables from the summed histograms; the stripe's bytes into d_out; returns their count"""
+        h = (ctypes.c_uint64 * STRIPE_HIST_WORDS)(*[int(x) for x in hist_sum])
+        n = ctypes.c_uint64()
+        _check(lib().dmmt_stripe_encode(self._ctx, h, d_out, out_cap, ctypes.byref(n)), "stripe_encode")
+        return int(n.value)
+
     def set_profiling(self, on: bool):
         _check(lib().dmmt_ctx_set_profiling(self._ctx, 1 if on else 0))
 
@@ -401,6 +444,39 @@ class Encoder:
         cnt = (ctypes.c_int32 * n)()
         _check(lib().dmmt_ctx_profile(self._ctx, ms, cnt, n))
         return {lib().dmmt_stage_name(i).decode(): (ms[i], cnt[i]) for i in range(n)}
+
+
+def stripe_rows(mcuy: int, world: int, rank: int, rows_per_interval: int = 1):
+    """MCU rows [row0, row0 + rows) of rank `rank` when `mcuy` MCU rows are split over
+    `world` GPUs in whole restart intervals of `rows_per_interval` rows."""
+    units = -(-mcuy // rows_per_interval)
+    lo = units * rank // world
+    hi = units * (rank + 1) // world
+    row0 = lo * rows_per_interval
+    return row0, min(hi * rows_per_interval, mcuy) - row0
+
+
+def encode_striped(enc: "Encoder", stripe: DmmtStripe, options: JpegTransformationOptions, d_out: int,
+                   out_cap: int, group=None):
+    """One image over the ranks of a torch.distributed group, one MCU-row stripe per
+    rank: the only exchange is an all-reduce of the 544 histogram
+    counters (the Huffman tables are global per image) and an all-gather of the
+    stripe sizes.  Returns (bytes of this stripe in d_out, its offset in the file,
+    file size); the stripes concatenated in rank order are the JPEG file."""
+    import torch
+    import torch.distributed as dist
+    hist = enc.stripe_analyze(stripe, options)
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    t = torch.from_numpy(hist.astype(np.int64)).to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    n = enc.stripe_encode(t.cpu().numpy().astype(np.uint64), d_out, out_cap)
+    sizes = torch.zeros(dist.get_world_size(group), dtype=torch.int64, device=dev)
+    mine = torch.tensor([n], dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes, mine, group=group)
+    sizes = sizes.cpu().tolist()
+    rank = dist.get_rank(group)
+    return n, int(sum(sizes[:rank])), int(sum(sizes))
 
 
 def max_jpeg_bytes(width: int, height: int, subsampling: int) -> int:
@@ -490,5 +566,6 @@ __all__ = [
     "Error", "LibraryMissing", "build", "lib", "ChromaSubsamplingPreset", "QuantizationTablePreset",
     "JpegTransformationOptions", "Image", "PPMImageReader", "Encoder", "JpegImageWriter", "Arguments",
     "convert_ppm_to_jpeg", "quantization_preset", "quality_tables", "max_jpeg_bytes", "device_count",
+    "DmmtStripe", "stripe_rows", "encode_striped",
     "AraiDiscrete8x8CosineTransformer", "encode_array", "io",
 ]

@@ -135,6 +135,32 @@ int dmmt_jpeg_encode_batch(dmmt_ctx* ctx, const dmmt_image* imgs, int n, const d
 int dmmt_encode_device(dmmt_ctx* ctx, const dmmt_device_frames* frames, const dmmt_options* opt, void* stream);
 size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t subsampling);
 
+/* ---- one image across several GPUs (extension) ---------------------------------------- */
+/* A run of whole MCU rows of one image (BASELINE config 4): with a restart
+ * interval (dmmt_options.restart_interval > 0) every stripe that starts and ends on an
+ * interval boundary encodes independently once the Huffman tables -- global per image --
+ * are known.  Protocol, one context per GPU:
+ *   dmmt_stripe_analyze  front half + the stripe's symbol histograms (host, uint64)
+ *   (exchange)           element-wise sum of every stripe's histograms
+ *   dmmt_stripe_encode   tables from the sum, the stripe's bytes: the JFIF header if it is
+ *                        the first stripe, its restart segments, then RSTm (more stripes
+ *                        follow) or EOI (the image ends)
+ * The stripes' outputs concatenated in row order are byte-identical to dmmt_jpeg_encode of
+ * the whole image with the same restart interval. */
+typedef struct dmmt_stripe {
+    const void* d_rgb;          /* device: the stripe's pixel rows only, interleaved R,G,B */
+    uint16_t width, height;     /* the whole image */
+    uint16_t maxval, sample_bytes;
+    int32_t mcu_row0, mcu_rows; /* MCU rows [mcu_row0, mcu_row0 + mcu_rows) */
+} dmmt_stripe;
+#define DMMT_STRIPE_HIST_WORDS (2 * (16 + 256)) /* [luma DC][luma AC][chroma DC][chroma AC] */
+int dmmt_stripe_analyze(dmmt_ctx* ctx, const dmmt_stripe* stripe, const dmmt_options* opt,
+                        uint64_t hist[DMMT_STRIPE_HIST_WORDS]);
+/* d_out: device buffer of out_cap >= dmmt_stripe_max_bytes bytes; *out_len (host) = bytes written */
+int dmmt_stripe_encode(dmmt_ctx* ctx, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS], uint8_t* d_out,
+                       size_t out_cap, uint64_t* out_len);
+size_t dmmt_stripe_max_bytes(const dmmt_stripe* stripe, const dmmt_options* opt);
+
 /* ---- stage-level entry points (parity tests) ---------------------------------------- */
 /* Front half only (transformer.rs:188-199): quantised zigzag blocks, MCU emission order
  * (block_fold_iterator.rs:53-148), 64 int16 per block, into coef (host). */
@@ -184,6 +210,9 @@ int dmmt_memcpy_d2h(dmmt_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* synthetic frames (SURVEY.md 8(d) generator) written straight into device memory */
 int dmmt_fill_synthetic(dmmt_ctx* ctx, void* d_rgb, uint16_t width, uint16_t height, int32_t n_frames,
                         int32_t first_frame, uint32_t seed);
+/* rows [row0, row0 + rows) of synthetic frame `frame` of a width x height image (a stripe) */
+int dmmt_fill_synthetic_rows(dmmt_ctx* ctx, void* d_rgb, uint16_t width, uint16_t height, int32_t row0,
+                             int32_t rows, int32_t frame, uint32_t seed);
 const char* dmmt_build_info(void);
 
 #ifdef __cplusplus
