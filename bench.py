@@ -44,6 +44,93 @@ CONFIGS = {
 }
 
 
+# one image over all ranks as MCU-row stripes (BASELINE config 4):
+# name: (width, height, subsampling, quality, MCU rows per restart interval)
+STRIPED = {
+    "32k420r": (32768, 32768, 2, 75, 1),
+}
+
+
+def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync):
+    """BASELINE config 4: one 32768x32768 image, MCU-row stripes (one per rank)
+    with a restart interval of one MCU row; per step every rank runs
+    dmmt_stripe_analyze, the 544-counter histogram all-reduce, dmmt_stripe_encode
+    and the all-gather of the stripe sizes (dmmt_jpeg.encode_striped).  Total work
+    is fixed: scaling "strong"; value = image pixels / MAX elapsed."""
+    w, h, sub, quality, rpi = STRIPED[args.config]
+    mcu_w, mcu_h = (8, 8) if sub == 0 else ((16, 8) if sub == 1 else (16, 16))
+    mcux, mcuy = -(-w // mcu_w), -(-h // mcu_h)
+    luma, chroma = dmmt_jpeg.quality_tables(quality)
+    opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
+                                               chroma_table=chroma, restart_interval=mcux * rpi)
+    enc = make_encoder(local_rank)
+    row0, rows = dmmt_jpeg.stripe_rows(mcuy, world, rank, rpi)
+    y0, y1 = row0 * mcu_h, min((row0 + rows) * mcu_h, h)
+    d_in = enc.malloc(w * (y1 - y0) * 3)
+    enc.fill_synthetic_rows(d_in, w, h, y0, y1 - y0, frame=0)
+    st = enc.stripe(d_in, w, h, row0, rows)
+    cap = enc.stripe_max_bytes(st, opts)
+    d_out = enc.malloc(cap)
+    if world == 1:
+        def step():
+            hist = enc.stripe_analyze(st, opts)
+            return enc.stripe_encode(hist, d_out, cap), 0, None
+    else:
+        def step():
+            return dmmt_jpeg.encode_striped(enc, st, opts, d_out, cap)
+    for _ in range(args.warmup):
+        step()
+    barrier_sync(enc)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n, off, total = step()
+    barrier_sync(enc)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=torch.device("cuda", local_rank) if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        cpu = None
+        if args.cpu_seconds > 0:  # the oracle on a bounded stripe of the same image (256 pixel rows)
+            from oracle.synth import synthetic
+            sample = synthetic(w, 256, frame=0)
+            cpu = cpu_baseline(sample, sub, luma, chroma, args.cpu_seconds)
+            cpu["sample"] = cpu["sample"].replace("frame(s) of the same synthetic workload",
+                                                  "pixel rows (the top stripe pattern) of the same synthetic image")
+        line = {
+            "metric": f"Mpixel/s encoded ({args.config}: one {w}x{h} image over {world} GPU(s))",
+            "value": round(w * h * args.steps / elapsed / 1e6, 2),
+            "unit": "Mpixel/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{w}x{h} synthetic RGB u8, {['4:4:4', '4:2:2', '4:2:0'][sub]}, IJG quality {quality}, "
+                            f"restart interval {mcux * rpi} MCUs, one MCU-row stripe per GPU, pixels in HBM -> "
+                            f"stripe bytes in HBM (histogram all-reduce + size all-gather per step)",
+                "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
+                "restart_interval": mcux * rpi, "parallelism": f"MCU-row stripes x{world}",
+                "jpeg_bytes": int(total) if total is not None else int(n),
+            },
+            "roofline": None,
+            "cpu_baseline": cpu,
+        }
+        emit(json.dumps(line))
+    enc.free(d_in)
+    enc.free(d_out)
+    enc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def stage_index(name):
     L = dmmt_jpeg.lib()
     for i in range(L.dmmt_num_stages()):
@@ -79,7 +166,7 @@ def main(argv=None, make_encoder=None, emit=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="4k444q90", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="4k444q90", choices=sorted(CONFIGS) + sorted(STRIPED))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--distinct-frames", type=int, default=4)
     args = ap.parse_args(argv)
@@ -103,6 +190,9 @@ def main(argv=None, make_encoder=None, emit=None):
         if dev is not None:
             torch.cuda.synchronize(dev)
         enc.synchronize()
+
+    if args.config in STRIPED:
+        return run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
 
     w, h, sub, quality, fps = CONFIGS[args.config]
     luma, chroma = dmmt_jpeg.quality_tables(quality)
