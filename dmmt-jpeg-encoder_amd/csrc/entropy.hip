@@ -43,10 +43,11 @@ static __device__ unsigned long long g_trace[64];
 
 static_assert(kChunkBlocks == 256, "one thread per block, one workgroup per chunk");
 
-// LDS word window of k_emit: 128 Ki bits = 512 bits per block on average (the 4K
-// q90 workload averages ~110).  A chunk with more is emitted in several windows,
-// every block re-walking its codes and keeping only the words inside the window.
-constexpr int kEmitWords = 4096;
+// LDS word window of k_emit: 64 Ki bits = 256 bits per block on average (the 4K
+// q90 workload averages ~110).  A chunk with more is assembled in several
+// windows, every block copying (or, on the re-walk path, re-emitting) only the
+// words inside the window.
+constexpr int kEmitWords = 2048;
 // Bytes per pass of k_stuffwrite (16 per thread).
 constexpr int kStuffPass = 4096;
 
@@ -167,6 +168,33 @@ struct WindowSink {
     }
 };
 
+// Private block slots of k_emit: every thread writes its block's bits MSB-first
+// from bit 0 of its own slot (no sharing, plain stores), word i of thread t at
+// sSlot[i * 256 + t] (consecutive threads, consecutive banks).  A block that needs
+// more than kSlotWords words sets `over`; the chunk then takes the re-walk path.
+constexpr int kSlotWords = 16;
+
+struct SlotSink {
+    uint32_t* slot;  // &sSlot[tid]
+    unsigned long long acc;
+    int nacc;
+    int wi;
+    __device__ __forceinline__ void operator()(uint32_t val, int len) {
+        acc = (acc << len) | val;
+        nacc += len;
+        if (nacc >= 32) {
+            nacc -= 32;
+            if (wi < kSlotWords) slot[wi * 256] = (uint32_t)(acc >> nacc);
+            ++wi;
+            acc &= (1ull << nacc) - 1ull;
+        }
+    }
+    __device__ __forceinline__ uint32_t finish() {
+        if (nacc > 0 && wi < kSlotWords) slot[wi * 256] = (uint32_t)(acc << (32 - nacc));
+        return (uint32_t)wi * 32u + (uint32_t)nacc;
+    }
+};
+
 // 16 bits of an MSB-first word stream starting at bit p (p & 31 taken; words a, b
 // hold bits from (p & ~31))
 __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
@@ -182,6 +210,7 @@ __global__ __launch_bounds__(256) void k_emit(const int16_t* coef, const int16_t
                                               uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist) {
     __shared__ uint32_t sTab[4 * 256];
     __shared__ uint32_t sW[kEmitWords + 2];
+    __shared__ uint32_t sSlot[kSlotWords * 256];
     __shared__ uint32_t sWave[4];
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
@@ -214,13 +243,16 @@ __global__ __launch_bounds__(256) void k_emit(const int16_t* coef, const int16_t
         }
         __syncthreads();
         DMMT_TRACE(0);
-        // bits of every block; offsets inside the chunk by a workgroup scan
+        // one walk: every block's bits into its private slot, and its bit count
         if (valid) {
-            CountSink cs;
-            walk_block(b, dcd, tb, tb + 256, cs);
-            bits = cs.n;
+            SlotSink ss{sSlot + tid, 0ull, 0, 0};
+            walk_block(b, dcd, tb, tb + 256, ss);
+            bits = ss.finish();
         }
     }
+    // offsets inside the chunk by a workgroup scan; a block too long for its slot
+    // sends the whole chunk down the re-walk path
+    const bool over = __syncthreads_or(bits > (uint32_t)kSlotWords * 32u) != 0;
     const uint32_t incl = wave_incl_scan_u32(bits);
     if (lane == 63) sWave[wave] = incl;
     __syncthreads();
@@ -238,13 +270,34 @@ __global__ __launch_bounds__(256) void k_emit(const int16_t* coef, const int16_t
         for (int i = tid; i <= wn; i += 256) sW[i] = 0u;  // + the next window's first word
         __syncthreads();
         if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
-            // the block again (L2 / MALL): holding it in registers across the scan
-            // would halve the occupancy of this kernel
-            BlockCoef b;
-            load_block(coef + e * 64, b);
-            WindowSink ws{sW, w0, wn + 1, 0ull, (int)(start & 31), (int)(start >> 5), true};
-            walk_block(b, dcd, tb, tb + 256, ws);
-            ws.finish();
+            if (!over) {
+                // shift the slot into place: destination word d of the window image
+                // gets the slot bits that land in it; the first and last word are
+                // shared with the neighbouring blocks (ORed), the rest are this
+                // block's alone
+                const int sh = (int)(start & 31);
+                const int d0 = (int)(start >> 5), d1 = (int)((start + bits - 1) >> 5);
+                const int nsw = (int)((bits + 31) >> 5);
+                for (int d = max(d0, w0); d <= min(d1, w0 + wn); ++d) {
+                    const int k = d - d0;  // slot word feeding the low part (k-1 feeds the high part)
+                    const uint32_t lo = k < nsw ? sSlot[k * 256 + tid] : 0u;
+                    const uint32_t hi = k > 0 ? sSlot[(k - 1) * 256 + tid] : 0u;
+                    const uint32_t v = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+                    if (d == d0 || d == d1)
+                        atomicOr(&sW[d - w0], v);
+                    else
+                        sW[d - w0] = v;
+                }
+            } else {
+                // the block again (L2 / MALL) and a second walk straight into the
+                // window: holding it in registers across the scan would halve the
+                // occupancy of this kernel
+                BlockCoef b;
+                load_block(coef + e * 64, b);
+                WindowSink ws{sW, w0, wn + 1, 0ull, (int)(start & 31), (int)(start >> 5), true};
+                walk_block(b, dcd, tb, tb + 256, ws);
+                ws.finish();
+            }
         }
         __syncthreads();
         for (int i = tid; i < wn; i += 256) {
