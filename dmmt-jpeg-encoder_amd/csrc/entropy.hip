@@ -467,6 +467,77 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
     const int per = (nch + 1023) / 1024;
     const int c0 = min(tid * per, nch), c1 = min(c0 + per, nch);
 
+    constexpr int KP = 2;
+    if (per <= KP) {  // uniform: every input of the chunk in registers before the scans
+        uint32_t nbits[KP], ffr[KP][8], edge[KP], nnext[KP], enext[KP];
+        bool first[KP], segl[KP];
+#pragma unroll
+        for (int i = 0; i < KP; ++i) {
+            const int c = c0 + i;
+            nbits[i] = edge[i] = nnext[i] = enext[i] = 0u;
+            first[i] = segl[i] = false;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) ffr[i][r] = 0u;
+            if (c < c1) {
+                const ChunkSpan sp = chunk_span(g, c);
+                first[i] = sp.seg_first;
+                segl[i] = sp.seg_last;
+                nbits[i] = cbits[c];
+                edge[i] = cedge[c];
+                const uint4 a = reinterpret_cast<const uint4*>(cff + (size_t)c * 8)[0];
+                const uint4 b = reinterpret_cast<const uint4*>(cff + (size_t)c * 8)[1];
+                ffr[i][0] = a.x, ffr[i][1] = a.y, ffr[i][2] = a.z, ffr[i][3] = a.w;
+                ffr[i][4] = b.x, ffr[i][5] = b.y, ffr[i][6] = b.z, ffr[i][7] = b.w;
+                if (!sp.seg_last) {
+                    nnext[i] = cbits[c + 1];
+                    enext[i] = cedge[c + 1];
+                }
+            }
+        }
+        bool f = false;
+        unsigned long long v = 0;
+#pragma unroll
+        for (int i = 0; i < KP; ++i)
+            if (c0 + i < c1) seg_combine(f, v, first[i], nbits[i]);
+        unsigned long long run = block_segscan_1024(f, v, sWave, sWaveF);
+        unsigned long long b0[KP], ob[KP], mine = 0;
+#pragma unroll
+        for (int i = 0; i < KP; ++i) {
+            const int c = c0 + i;
+            b0[i] = ob[i] = 0;
+            if (c >= c1) continue;
+            if (first[i]) run = 0;
+            b0[i] = run;
+            const unsigned long long e = run + nbits[i];
+            unsigned long long o = ((e + 7) >> 3) - ((run + 7) >> 3);
+            const int rsd = (8 - (int)(run & 7)) & 7;
+            uint32_t ffc = 0;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) ffc = r == rsd ? ffr[i][r] : ffc;
+            o += ffc;
+            if ((e & 7) && (e & ~7ull) >= run) {
+                const uint32_t byte = boundary_byte((int)(e & 7), edge[i] & 0xFFFFu, !segl[i], nnext[i], enext[i] >> 16);
+                o += byte == 0xFFu ? 1u : 0u;
+            }
+            if (segl[i] && (c != nch - 1 || g.more_after)) o += 2;  // RSTm (extension)
+            ob[i] = o;
+            mine += o;
+            run = e;
+        }
+        unsigned long long tot = 0;
+        unsigned long long orun = block_scan_1024(mine, sWave, &tot);
+#pragma unroll
+        for (int i = 0; i < KP; ++i) {
+            const int c = c0 + i;
+            if (c >= c1) continue;
+            bit0[c] = b0[i];
+            outo[c] = orun;
+            orun += ob[i];
+        }
+        if (tid == 0) total_out[frame] = tot;
+        return;
+    }
+
     // bit offsets inside the restart segments: segmented scan of the chunk bits
     bool f = false;
     unsigned long long v = 0;
