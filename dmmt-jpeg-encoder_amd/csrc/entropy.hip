@@ -561,7 +561,7 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
 }
 
 // ----------------------------------------------------------------- k_stuffwrite
-__global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__ stage,
+__global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restrict__ stage,
                                                     const uint32_t* __restrict__ chunk_bits,
                                                     const uint32_t* __restrict__ chunk_edge,
                                                     const unsigned long long* __restrict__ chunk_bit0,
@@ -619,9 +619,10 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
     uint8_t* o = base + chunk_out[cid];
     for (unsigned long long pos = 0; pos < nbytes; pos += kStuffPass) {  // uniform
         const unsigned long long kb = pos + 16u * (unsigned)tid;          // first of my 16 bytes (chunk-relative)
-        uint8_t v[16];
+        const int nvalid = kb < nbytes ? (int)min(16ull, nbytes - kb) : 0;
+        uint32_t x[4] = {0u, 0u, 0u, 0u};  // my 16 bytes, MSB first
         uint32_t cnt = 0;
-        if (kb < nbytes) {
+        if (nvalid) {
             const unsigned long long p = off + 8 * kb;  // bit position in the chunk stream
             const size_t wi = (size_t)(p >> 5);
             const int sh = (int)(p & 31);
@@ -629,15 +630,18 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
 #pragma unroll
             for (int i = 0; i < 5; ++i) wv[i] = slot[wi + i];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t x = sh ? (wv[i] << sh) | (wv[i + 1] >> (32 - sh)) : wv[i];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[4 * i + j] = (uint8_t)(x >> (24 - 8 * j));
+            for (int i = 0; i < 4; ++i) x[i] = sh ? (wv[i] << sh) | (wv[i + 1] >> (32 - sh)) : wv[i];
+            if (shared_tail && nbytes - 1 - kb < 16) {  // the shared / padded last byte
+                const int j = (int)(nbytes - 1 - kb), sft = 24 - 8 * (j & 3);
+                x[j >> 2] = (x[j >> 2] & ~(0xFFu << sft)) | (tail << sft);
             }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                if (shared_tail && kb + j == nbytes - 1) v[j] = (uint8_t)tail;
-                cnt += (kb + j < nbytes && v[j] == 0xFF) ? 1u : 0u;
+            for (int i = 0; i < 4; ++i) {  // 0xFF bytes among the valid ones
+                const int nv = min(max(nvalid - 4 * i, 0), 4);
+                const uint32_t vmask = nv ? 0x80808080u & (0xFFFFFFFFu << (32 - 8 * nv)) : 0u;
+                const uint32_t t = ~x[i];
+                const uint32_t nonzero = (((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+                cnt += (uint32_t)__popc(~nonzero & vmask);
             }
         }
         const uint32_t incl = wave_incl_scan_u32(cnt);
@@ -648,13 +652,14 @@ __global__ __launch_bounds__(256) void k_stuffwrite(const uint32_t* __restrict__
         const uint32_t ffs = sWave[0] + sWave[1] + sWave[2] + sWave[3];
         // stage the stuffed pass in LDS, then store it with consecutive lanes on
         // consecutive bytes (coalesced)
-        if (kb < nbytes) {
+        if (nvalid) {
             uint32_t dst = (uint32_t)tid * 16u + pre;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                if (kb + j < nbytes) {
-                    sOut[dst++] = v[j];
-                    if (v[j] == 0xFF) sOut[dst++] = 0x00;
+                if (j < nvalid) {
+                    const uint32_t b = (x[j >> 2] >> (24 - 8 * (j & 3))) & 0xFFu;
+                    sOut[dst++] = (uint8_t)b;
+                    if (b == 0xFFu) sOut[dst++] = 0x00;
                 }
             }
         }
