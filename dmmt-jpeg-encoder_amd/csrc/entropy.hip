@@ -43,11 +43,11 @@ static __device__ unsigned long long g_trace[64];
 
 static_assert(kChunkBlocks == 256, "one thread per block, one workgroup per chunk");
 
-// LDS word window of k_emit: 64 Ki bits = 256 bits per block on average (the 4K
+// LDS word window of k_emit: 32 Ki bits = 128 bits per block on average (the 4K
 // q90 workload averages ~110).  A chunk with more is assembled in several
 // windows, every block copying (or, on the re-walk path, re-emitting) only the
 // words inside the window.
-constexpr int kEmitWords = 2048;
+constexpr int kEmitWords = 1024;
 // Bytes per pass of k_stuffwrite (16 per thread).
 constexpr int kStuffPass = 4096;
 
@@ -171,8 +171,9 @@ struct WindowSink {
 // Private block slots of k_emit: every thread writes its block's bits MSB-first
 // from bit 0 of its own slot (no sharing, plain stores), word i of thread t at
 // sSlot[i * 256 + t] (consecutive threads, consecutive banks).  A block that needs
-// more than kSlotWords words sets `over`; the chunk then takes the re-walk path.
-constexpr int kSlotWords = 16;
+// more than kSlotWords words (384 bits) sets `over`; the chunk then takes the
+// re-walk path.  Small slots and window keep 7 workgroups resident per CU.
+constexpr int kSlotWords = 12;
 
 struct SlotSink {
     uint32_t* slot;  // &sSlot[tid]
@@ -203,7 +204,7 @@ __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
 }
 
 // ---------------------------------------------------------------------- k_emit
-__global__ __launch_bounds__(256) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
+__global__ __launch_bounds__(256, 8) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
                                               const uint32_t* __restrict__ code_tab, Geom g,
                                               uint32_t* __restrict__ stage, uint32_t* __restrict__ chunk_bits,
                                               uint32_t* __restrict__ chunk_ff, uint32_t* __restrict__ chunk_edge,
