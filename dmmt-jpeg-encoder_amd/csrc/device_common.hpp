@@ -10,10 +10,13 @@ namespace dmmt {
 // workgroup accumulates, in registers, the 100-MHz real-time ticks and the
 // shader-clock cycles between consecutive marks per phase slot (< 16) and adds
 // them to the translation unit's g_trace (slots i, 16+i; 32+i counts the marks)
-// once, at DMMT_TRACE_FLUSH.  Compiled out of the product library.
+// once, at DMMT_TRACE_FLUSH.  Span slot s (48+4s..51+4s) keeps ~(first start),
+// last end, summed workgroup lifetimes and the workgroup count, so a per-launch
+// readout gives the dispatch spread.  Compiled out of the product library.
 #ifdef DMMT_PHASE_TRACE
 #define DMMT_TRACE_START                                                  \
     unsigned long long _dmmt_tr = __builtin_amdgcn_s_memrealtime();       \
+    const unsigned long long _dmmt_t0 = _dmmt_tr;                         \
     unsigned long long _dmmt_tc = __builtin_amdgcn_s_memtime();           \
     unsigned long long _dmmt_acc[16], _dmmt_clk[16];                      \
     unsigned _dmmt_cnt[16];                                               \
@@ -32,9 +35,14 @@ namespace dmmt {
         _dmmt_tr = _n;                                                    \
         _dmmt_tc = _c;                                                    \
     } while (0)
-#define DMMT_TRACE_FLUSH(base)                                            \
+#define DMMT_TRACE_FLUSH(base, span)                                      \
     do {                                                                  \
         if (threadIdx.x == 0) {                                           \
+            const unsigned long long _e = __builtin_amdgcn_s_memrealtime(); \
+            atomicMax(&g_trace[48 + 4 * (span)], ~_dmmt_t0);              \
+            atomicMax(&g_trace[49 + 4 * (span)], _e);                     \
+            atomicAdd(&g_trace[50 + 4 * (span)], _e - _dmmt_t0);          \
+            atomicAdd(&g_trace[51 + 4 * (span)], 1ull);                   \
             _Pragma("unroll") for (int _i = 0; _i < 16; ++_i) if (_dmmt_cnt[_i]) { \
                 atomicAdd(&g_trace[(base) + _i], _dmmt_acc[_i]);          \
                 atomicAdd(&g_trace[16 + (base) + _i], _dmmt_clk[_i]);     \
@@ -49,7 +57,7 @@ namespace dmmt {
 #define DMMT_TRACE(i) \
     do {              \
     } while (0)
-#define DMMT_TRACE_FLUSH(base) \
+#define DMMT_TRACE_FLUSH(base, span) \
     do {                       \
     } while (0)
 #endif

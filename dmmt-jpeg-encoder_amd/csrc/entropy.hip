@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256, 8) void k_emit(const int16_t* coef, const int1
         chunk_edge[cid] = (first16 << 16) | last16;
     }
     DMMT_TRACE(3);
-    DMMT_TRACE_FLUSH(0);
+    DMMT_TRACE_FLUSH(0, 0);
 }
 
 // The byte that starts m1 (1..7) bits before the end of a chunk: those last m1

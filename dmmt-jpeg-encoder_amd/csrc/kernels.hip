@@ -25,6 +25,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "device_common.hpp"
 #include "jpeg_common.hpp"
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
         if (v) atomicAdd(&gh[i], v);
     }
     DMMT_TRACE(5);
-    DMMT_TRACE_FLUSH(0);
+    DMMT_TRACE_FLUSH(0, 0);
 }
 
 // ============================================================== k_dcdiff
@@ -826,7 +827,7 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
         }
     }
     DMMT_TRACE(15);
-    DMMT_TRACE_FLUSH(0);
+    DMMT_TRACE_FLUSH(0, 1);
 }
 
 // ============================================================== operator: DCT only
@@ -960,6 +961,7 @@ static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
             cus = 256;
+        if (const char* e = getenv("DMMT_FRONT_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning knob
         resident = per_cu * cus;
     }
     dim3 grid(clampi(ntiles, 1, resident / n_frames > 0 ? resident / n_frames : 1), n_frames);

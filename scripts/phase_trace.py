@@ -48,17 +48,33 @@ def main():
     enc.synchronize()
     for tu in ("kernels", "entropy"):
         getattr(L, f"dmmt_debug_trace_{tu}")(buf)
-    for _ in range(args.steps):
+    acc = {tu: [0] * 48 for tu in ("kernels", "entropy")}
+    spans = {tu: [[0.0, 0.0, 0] for _ in range(4)] for tu in ("kernels", "entropy")}
+    for _ in range(args.steps):  # one readout per step: the span slots hold per-launch extrema
         enc.encode_device(d_in, fps, w, h, None, d_out, out_stride, d_len, frame_stride=w * h * 3, opt_c=opt_c)
-    enc.synchronize()
+        enc.synchronize()
+        for tu in ("kernels", "entropy"):
+            getattr(L, f"dmmt_debug_trace_{tu}")(buf)
+            v = list(buf)
+            for i in range(48):
+                acc[tu][i] += v[i]
+            for s in range(4):
+                t0, t1, life, n = (~v[48 + 4 * s]) & (2**64 - 1), v[49 + 4 * s], v[50 + 4 * s], v[51 + 4 * s]
+                if n:
+                    spans[tu][s][0] += (t1 - t0) / 100
+                    spans[tu][s][1] += life / n / 100
+                    spans[tu][s][2] = n
     for tu in ("kernels", "entropy"):
-        getattr(L, f"dmmt_debug_trace_{tu}")(buf)
-        v = list(buf)
+        v = acc[tu]
         for i in range(16):
             if v[32 + i]:
                 print(f"{tu:8s} {i:2d} {NAMES[tu].get(i, '?'):22s} marks/step={v[32 + i] / args.steps:9.1f} "
                       f"us/mark={v[i] / v[32 + i] / 100:9.3f} us/step(sum over marks)={v[i] / args.steps / 100:12.1f} "
                       f"clock={v[16 + i] / max(v[i], 1) * 100:6.0f} MHz")
+        for s in range(4):
+            if spans[tu][s][2]:
+                print(f"{tu:8s} span {s}: workgroups={spans[tu][s][2]} first start->last end="
+                      f"{spans[tu][s][0] / args.steps:8.2f} us  mean workgroup lifetime={spans[tu][s][1] / args.steps:8.2f} us")
     enc.close()
 
 
