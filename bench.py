@@ -46,17 +46,21 @@ CONFIGS = {
 
 # one image over all ranks as MCU-row stripes (BASELINE config 4):
 # name: (width, height, subsampling, quality, MCU rows per restart interval)
-STRIPED = {
+STRIPED = {  # (width, height, subsampling, quality, MCU rows per restart interval; 0 = none, joined stripes)
     "32k420r": (32768, 32768, 2, 75, 1),
+    "32k420": (32768, 32768, 2, 75, 0),
 }
 
 
 def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync):
-    """BASELINE config 4: one 32768x32768 image, MCU-row stripes (one per rank)
-    with a restart interval of one MCU row; per step every rank runs
+    """BASELINE config 4: one 32768x32768 image, MCU-row stripes (one per rank).
+    "32k420r": a restart interval of one MCU row; per step every rank runs
     dmmt_stripe_analyze, the 544-counter histogram all-reduce, dmmt_stripe_encode
-    and the all-gather of the stripe sizes (dmmt_jpeg.encode_striped).  Total work
-    is fixed: scaling "strong"; value = image pixels / MAX elapsed."""
+    and the all-gather of the stripe sizes (dmmt_jpeg.encode_striped).  "32k420":
+    no restart intervals (the reference's own stream, joined stripes): analyze,
+    edge-DC all-gather, histogram all-reduce, measure, (bits, head) all-gather,
+    write.  Total work is fixed: scaling "strong"; value = image pixels / MAX
+    elapsed."""
     w, h, sub, quality, rpi = STRIPED[args.config]
     mcu_w, mcu_h = (8, 8) if sub == 0 else ((16, 8) if sub == 1 else (16, 16))
     mcux, mcuy = -(-w // mcu_w), -(-h // mcu_h)
@@ -64,14 +68,19 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
     opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
                                                chroma_table=chroma, restart_interval=mcux * rpi)
     enc = make_encoder(local_rank)
-    row0, rows = dmmt_jpeg.stripe_rows(mcuy, world, rank, rpi)
+    row0, rows = dmmt_jpeg.stripe_rows(mcuy, world, rank, max(rpi, 1))
     y0, y1 = row0 * mcu_h, min((row0 + rows) * mcu_h, h)
     d_in = enc.malloc(w * (y1 - y0) * 3)
     enc.fill_synthetic_rows(d_in, w, h, y0, y1 - y0, frame=0)
     st = enc.stripe(d_in, w, h, row0, rows)
     cap = enc.stripe_max_bytes(st, opts)
     d_out = enc.malloc(cap)
-    if world == 1:
+    if world == 1 and rpi == 0:
+        def step():
+            hist = enc.stripe_analyze(st, opts)
+            enc.stripe_measure(hist, [0, 0, 0], d_out, cap)
+            return enc.stripe_write(0, 0, 0), 0, None
+    elif world == 1:
         def step():
             hist = enc.stripe_analyze(st, opts)
             return enc.stripe_encode(hist, d_out, cap), 0, None
@@ -114,8 +123,11 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
             "data": "synthetic",
             "config": {
                 "workload": f"{w}x{h} synthetic RGB u8, {['4:4:4', '4:2:2', '4:2:0'][sub]}, IJG quality {quality}, "
-                            f"restart interval {mcux * rpi} MCUs, one MCU-row stripe per GPU, pixels in HBM -> "
-                            f"stripe bytes in HBM (histogram all-reduce + size all-gather per step)",
+                            + (f"restart interval {mcux * rpi} MCUs, one MCU-row stripe per GPU, pixels in HBM -> "
+                               f"stripe bytes in HBM (histogram all-reduce + size all-gather per step)" if rpi else
+                               "no restart intervals (the reference's stream), one MCU-row stripe per GPU joined "
+                               "mid-byte, pixels in HBM -> stripe bytes in HBM (edge-DC all-gather, histogram "
+                               "all-reduce, bit-count all-gather, size all-gather per step)"),
                 "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
                 "restart_interval": mcux * rpi, "parallelism": f"MCU-row stripes x{world}",
                 "jpeg_bytes": int(total) if total is not None else int(n),

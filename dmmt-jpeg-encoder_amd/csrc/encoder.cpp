@@ -75,6 +75,11 @@ struct dmmt_ctx {
     Geom stripe_g{};
     dmmt_options stripe_opt{};
     int stripe_sb = 1;
+    // joined stripes (restart_interval 0): DC edges from analyze, output from measure
+    int16_t stripe_dc_first[3] = {0, 0, 0}, stripe_dc_last[3] = {0, 0, 0};
+    bool stripe_measured = false;
+    uint8_t* stripe_out = nullptr;
+    size_t stripe_cap = 0;
 };
 
 namespace {
@@ -791,21 +796,21 @@ static int stripe_geom(const dmmt_stripe* st, const dmmt_options* opt, Geom* g) 
     if (!st || !opt || !st->d_rgb) return DMMT_E_INVALID_ARGUMENT;
     if (st->sample_bytes != 1 && st->sample_bytes != 2 && st->sample_bytes != 4) return DMMT_E_INVALID_ARGUMENT;
     const int ri = opt->restart_interval;
-    if (ri <= 0) return DMMT_E_INVALID_ARGUMENT;  // stripes are restart segments
+    if (ri < 0) return DMMT_E_INVALID_ARGUMENT;  // 0: joined stripes, > 0: restart segments
     Geom full;
     int rc;
     if ((rc = make_checked_geom(st->width, st->height, opt->subsampling, st->maxval, ri, &full))) return rc;
     if (st->mcu_row0 < 0 || st->mcu_rows <= 0 || st->mcu_row0 + st->mcu_rows > full.mcuy) return DMMT_E_INVALID_ARGUMENT;
     const long long m0 = (long long)st->mcu_row0 * full.mcux;
     const bool last = st->mcu_row0 + st->mcu_rows == full.mcuy;
-    if (m0 % ri) return DMMT_E_INVALID_ARGUMENT;  // must start a restart interval
-    if (!last && ((long long)st->mcu_rows * full.mcux) % ri) return DMMT_E_INVALID_ARGUMENT;  // and end one
+    if (ri > 0 && m0 % ri) return DMMT_E_INVALID_ARGUMENT;  // must start a restart interval
+    if (ri > 0 && !last && ((long long)st->mcu_rows * full.mcux) % ri) return DMMT_E_INVALID_ARGUMENT;  // and end one
     const int rows_px = 8 * full.vr;
     const int y0 = st->mcu_row0 * rows_px;
     const int h = std::min(st->mcu_rows * rows_px, (int)st->height - y0);
     *g = make_geom(st->width, h, opt->subsampling, st->maxval, ri);
     g->sof_height = st->height;
-    g->seg_base = (int)(m0 / ri);
+    g->seg_base = ri > 0 ? (int)(m0 / ri) : 0;
     g->stripe_first = st->mcu_row0 == 0;
     g->more_after = !last;
     return DMMT_OK;
@@ -856,26 +861,29 @@ extern "C" int dmmt_stripe_analyze(dmmt_ctx* c, const dmmt_stripe* st, const dmm
             hist[288 + k] += ac[(size_t)r * 512 + 256 + k];
         }
     }
+    if (g.restart_interval == 0) {  // joined stripes: DC edges for the neighbours' predictors
+        int16_t head[8], tail[8];
+        const int bpm = g.bpm, nl = g.n_luma;
+        HIP_TRY(hipMemcpyAsync(head, w.dc, bpm * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(tail, w.dc + (g.bpf - bpm), bpm * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        c->stripe_dc_first[0] = head[0];  // the stripe's first Y, Cb, Cr blocks (emission order)
+        c->stripe_dc_first[1] = head[nl];
+        c->stripe_dc_first[2] = head[nl + 1];
+        c->stripe_dc_last[0] = tail[nl - 1];  // and its last ones
+        c->stripe_dc_last[1] = tail[nl];
+        c->stripe_dc_last[2] = tail[nl + 1];
+    }
     c->stripe_g = g;
     c->stripe_opt = *opt;
     c->stripe_sb = st->sample_bytes;
     c->stripe_pending = true;
+    c->stripe_measured = false;
     return DMMT_OK;
 }
 
-extern "C" int dmmt_stripe_encode(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS], uint8_t* d_out,
-                                  size_t out_cap, uint64_t* out_len) {
-    if (!c || !hist_sum || !d_out || !out_len) return DMMT_E_INVALID_ARGUMENT;
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (!c->stripe_pending) return DMMT_E_INVALID_ARGUMENT;  // dmmt_stripe_analyze first
-    int rc;
-    if ((rc = set_device(c))) return rc;
-    const Geom g = c->stripe_g;
-    if (out_cap < max_jpeg_bytes(g)) return DMMT_E_CAPACITY;
-    hipStream_t s = c->stream;
-    Work w;
-    if ((rc = prepare(c, g, 1, &c->stripe_opt, c->stripe_sb, s, &w))) return rc;
-    // the summed histograms go into replica 0 (the other replicas are zero)
+// upload the summed [luma DC][luma AC][chroma DC][chroma AC] counters into replica 0
+static int upload_hist_sum(const Work& w, const uint64_t* hist_sum, hipStream_t s) {
     std::vector<uint32_t> ac(512), dc(32);
     for (int k = 0; k < 16; ++k) {
         if (hist_sum[k] > 0xFFFFFFFFull || hist_sum[272 + k] > 0xFFFFFFFFull) return DMMT_E_INVALID_ARGUMENT;
@@ -889,6 +897,147 @@ extern "C" int dmmt_stripe_encode(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRI
     }
     HIP_TRY(hipMemcpyAsync(w.ac_hist, ac.data(), ac.size() * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(w.dc_hist, dc.data(), dc.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the host vectors go out of scope
+    return DMMT_OK;
+}
+
+// categorize.rs:22-74: bit length of |v|
+static int dc_category(int v) {
+    unsigned a = (unsigned)(v < 0 ? -v : v);
+    int n = 0;
+    while (a) {
+        ++n;
+        a >>= 1;
+    }
+    return n;
+}
+
+extern "C" int dmmt_stripe_dc_edges(dmmt_ctx* c, int16_t first_dc[3], int16_t last_dc[3]) {
+    if (!c || !first_dc || !last_dc) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stripe_pending || c->stripe_g.restart_interval != 0) return DMMT_E_INVALID_ARGUMENT;
+    for (int i = 0; i < 3; ++i) {
+        first_dc[i] = c->stripe_dc_first[i];
+        last_dc[i] = c->stripe_dc_last[i];
+    }
+    return DMMT_OK;
+}
+
+extern "C" void dmmt_stripe_fix_dc_hist(uint64_t hist[DMMT_STRIPE_HIST_WORDS], const int16_t first_dc[3],
+                                        const int16_t prev_last_dc[3]) {
+    for (int i = 0; i < 3; ++i) {  // luma DC at 0, chroma (Cb and Cr) DC at 272
+        uint64_t* h = hist + (i == 0 ? 0 : 272);
+        const int was = dc_category(first_dc[i]);
+        const int is = dc_category((int16_t)(first_dc[i] - prev_last_dc[i]));  // categorize.rs:153-169, i16
+        if (h[was] > 0) {
+            h[was] -= 1;
+            h[is] += 1;
+        }
+    }
+}
+
+extern "C" int dmmt_stripe_measure(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS],
+                                   const int16_t prev_last_dc[3], uint8_t* d_out, size_t out_cap, uint64_t* bits,
+                                   uint32_t* first16) {
+    if (!c || !hist_sum || !prev_last_dc || !d_out || !bits || !first16) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stripe_pending || c->stripe_g.restart_interval != 0) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const Geom g = c->stripe_g;
+    if (out_cap < max_jpeg_bytes(g)) return DMMT_E_CAPACITY;
+    hipStream_t s = c->stream;
+    Work w;
+    if ((rc = prepare(c, g, 1, &c->stripe_opt, c->stripe_sb, s, &w))) return rc;
+    if ((rc = upload_hist_sum(w, hist_sum, s))) return rc;
+    // the stripe's first DC differences continue the previous stripe's predictors
+    int16_t d[3];
+    const long long at[3] = {0, g.n_luma, g.n_luma + 1};
+    for (int i = 0; i < 3; ++i) {
+        d[i] = (int16_t)(c->stripe_dc_first[i] - prev_last_dc[i]);
+        HIP_TRY(hipMemcpyAsync(w.dcdiff + at[i], &d[i], sizeof(int16_t), hipMemcpyHostToDevice, s));
+    }
+    {
+        StageTimer t(c, ST_TABLES, s);
+        HIP_TRY(launch_tables(1, g, w, c->stripe_opt.bits_per_channel, d_out, out_cap, s));
+    }
+    {
+        StageTimer t(c, ST_EMIT, s);
+        HIP_TRY(launch_emit(1, g, w, s));
+    }
+    std::vector<uint32_t> nb((size_t)g.nch), edge((size_t)g.nch);
+    HIP_TRY(hipMemcpyAsync(nb.data(), w.chunk_bits, nb.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(edge.data(), w.chunk_edge, edge.size() * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if ((rc = take_status(c, s))) return rc;
+    uint64_t total = 0;
+    uint32_t f = 0;
+    int have = 0;
+    for (int k = 0; k < g.nch; ++k) {
+        if (have < 16 && nb[k]) {  // the scan's first 16 bits, across chunks shorter than that
+            const int t = std::min(16 - have, (int)std::min<uint32_t>(nb[k], 16u));
+            f |= ((edge[k] >> 16) >> (16 - t)) << (16 - have - t);
+            have += t;
+        }
+        total += nb[k];
+    }
+    *bits = total;
+    *first16 = f;
+    c->stripe_out = d_out;
+    c->stripe_cap = out_cap;
+    c->stripe_measured = true;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_stripe_write(dmmt_ctx* c, uint64_t bit_offset, uint32_t next_bits, uint32_t next16,
+                                 uint64_t* out_len) {
+    if (!c || !out_len || next_bits > 16) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stripe_pending || !c->stripe_measured) return DMMT_E_INVALID_ARGUMENT;  // dmmt_stripe_measure first
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    Geom g = c->stripe_g;
+    if (g.stripe_first && bit_offset) return DMMT_E_INVALID_ARGUMENT;
+    g.bit_phase = (int)(bit_offset & 7);
+    g.next_bits = g.more_after ? (int)next_bits : 0;
+    g.next16 = g.more_after ? (next16 & 0xFFFFu) & ~(0xFFFFu >> next_bits) : 0u;
+    hipStream_t s = c->stream;
+    Work w;
+    if ((rc = prepare(c, g, 1, &c->stripe_opt, c->stripe_sb, s, &w))) return rc;
+    if ((rc = ensure(c->out_len, 4))) return rc;
+    {
+        StageTimer t(c, ST_OFFSETS, s);
+        HIP_TRY(launch_offsets(1, g, w, s));
+    }
+    {
+        StageTimer t(c, ST_STUFFWRITE, s);
+        HIP_TRY(launch_stuffwrite(1, g, w, c->stripe_out, c->stripe_cap, (uint32_t*)c->out_len.p, s));
+    }
+    uint32_t len = 0;
+    HIP_TRY(hipMemcpyAsync(&len, c->out_len.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    c->stripe_pending = false;
+    c->stripe_measured = false;
+    if ((rc = take_status(c, s))) return rc;
+    *out_len = len;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_stripe_encode(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS], uint8_t* d_out,
+                                  size_t out_cap, uint64_t* out_len) {
+    if (!c || !hist_sum || !d_out || !out_len) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->stripe_pending) return DMMT_E_INVALID_ARGUMENT;  // dmmt_stripe_analyze first
+    if (c->stripe_g.restart_interval == 0) return DMMT_E_INVALID_ARGUMENT;  // joined: measure + write
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    const Geom g = c->stripe_g;
+    if (out_cap < max_jpeg_bytes(g)) return DMMT_E_CAPACITY;
+    hipStream_t s = c->stream;
+    Work w;
+    if ((rc = prepare(c, g, 1, &c->stripe_opt, c->stripe_sb, s, &w))) return rc;
+    // the summed histograms go into replica 0 (the other replicas are zero)
+    if ((rc = upload_hist_sum(w, hist_sum, s))) return rc;
     if ((rc = ensure(c->out_len, 4))) return rc;
     if ((rc = enqueue_back_half(c, g, 1, w, c->stripe_opt.bits_per_channel, d_out, out_cap, (uint32_t*)c->out_len.p,
                                 s, true)))

@@ -73,6 +73,12 @@ __device__ __forceinline__ ChunkSpan chunk_span(const Geom& g, int c) {
     return r;
 }
 
+// The frame's last chunk of a joined stripe (no restart intervals, more stripes
+// follow): its last byte runs on into the next stripe's first bits (g.next16).
+__device__ __forceinline__ bool joined_tail(const Geom& g, int c) {
+    return c == g.nch - 1 && g.more_after && g.restart_interval == 0;
+}
+
 // One thread walks one block (64 zigzag coefficients held in 32 registers) in
 // stream order (encoder.rs:356-404; categorize.rs:132-169): DC code + extra bits,
 // then for each non-zero AC coefficient (run >> 4) ZRL codes and
@@ -204,7 +210,7 @@ __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
 }
 
 // ---------------------------------------------------------------------- k_emit
-__global__ __launch_bounds__(256, 8) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
+__global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
                                               const uint32_t* __restrict__ code_tab, Geom g,
                                               uint32_t* __restrict__ stage, uint32_t* __restrict__ chunk_bits,
                                               uint32_t* __restrict__ chunk_ff, uint32_t* __restrict__ chunk_edge,
@@ -375,12 +381,14 @@ __device__ __forceinline__ unsigned long long chunk_out_bytes(const uint32_t* __
     unsigned long long out = ((e + 7) >> 3) - ((b0 + 7) >> 3);
     out += cff[(size_t)c * 8 + ((8 - (b0 & 7)) & 7)];
     if ((e & 7) && (e & ~7ull) >= b0) {
-        const bool has_next = !sp.seg_last;
-        const uint32_t byte = boundary_byte((int)(e & 7), cedge[c] & 0xFFFFu, has_next, has_next ? cbits[c + 1] : 0u,
-                                            has_next ? cedge[c + 1] >> 16 : 0u);
+        const bool jt = joined_tail(g, c);
+        const bool has_next = !sp.seg_last || jt;
+        const uint32_t nn = jt ? (uint32_t)g.next_bits : (has_next ? cbits[c + 1] : 0u);
+        const uint32_t fn = jt ? g.next16 : (has_next ? cedge[c + 1] >> 16 : 0u);
+        const uint32_t byte = boundary_byte((int)(e & 7), cedge[c] & 0xFFFFu, has_next, nn, fn);
         out += byte == 0xFFu ? 1u : 0u;
     }
-    if (sp.seg_last && (c != g.nch - 1 || g.more_after)) out += 2;  // RSTm (extension)
+    if (sp.seg_last && (c != g.nch - 1 || (g.more_after && g.restart_interval > 0))) out += 2;  // RSTm (extension)
     return out;
 }
 
@@ -471,18 +479,19 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
     constexpr int KP = 2;
     if (per <= KP) {  // uniform: every input of the chunk in registers before the scans
         uint32_t nbits[KP], ffr[KP][8], edge[KP], nnext[KP], enext[KP];
-        bool first[KP], segl[KP];
+        bool first[KP], segl[KP], hasn[KP];
 #pragma unroll
         for (int i = 0; i < KP; ++i) {
             const int c = c0 + i;
             nbits[i] = edge[i] = nnext[i] = enext[i] = 0u;
-            first[i] = segl[i] = false;
+            first[i] = segl[i] = hasn[i] = false;
 #pragma unroll
             for (int r = 0; r < 8; ++r) ffr[i][r] = 0u;
             if (c < c1) {
                 const ChunkSpan sp = chunk_span(g, c);
                 first[i] = sp.seg_first;
                 segl[i] = sp.seg_last;
+                hasn[i] = !sp.seg_last;
                 nbits[i] = cbits[c];
                 edge[i] = cedge[c];
                 const uint4 a = reinterpret_cast<const uint4*>(cff + (size_t)c * 8)[0];
@@ -492,6 +501,10 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
                 if (!sp.seg_last) {
                     nnext[i] = cbits[c + 1];
                     enext[i] = cedge[c + 1];
+                } else if (joined_tail(g, c)) {
+                    hasn[i] = true;
+                    nnext[i] = (uint32_t)g.next_bits;
+                    enext[i] = g.next16 << 16;
                 }
             }
         }
@@ -499,7 +512,7 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
         unsigned long long v = 0;
 #pragma unroll
         for (int i = 0; i < KP; ++i)
-            if (c0 + i < c1) seg_combine(f, v, first[i], nbits[i]);
+            if (c0 + i < c1) seg_combine(f, v, first[i], nbits[i] + (c0 + i == 0 ? (uint32_t)g.bit_phase : 0u));
         unsigned long long run = block_segscan_1024(f, v, sWave, sWaveF);
         unsigned long long b0[KP], ob[KP], mine = 0;
 #pragma unroll
@@ -507,7 +520,7 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
             const int c = c0 + i;
             b0[i] = ob[i] = 0;
             if (c >= c1) continue;
-            if (first[i]) run = 0;
+            if (first[i]) run = c == 0 ? (unsigned long long)g.bit_phase : 0ull;
             b0[i] = run;
             const unsigned long long e = run + nbits[i];
             unsigned long long o = ((e + 7) >> 3) - ((run + 7) >> 3);
@@ -517,10 +530,10 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
             for (int r = 0; r < 8; ++r) ffc = r == rsd ? ffr[i][r] : ffc;
             o += ffc;
             if ((e & 7) && (e & ~7ull) >= run) {
-                const uint32_t byte = boundary_byte((int)(e & 7), edge[i] & 0xFFFFu, !segl[i], nnext[i], enext[i] >> 16);
+                const uint32_t byte = boundary_byte((int)(e & 7), edge[i] & 0xFFFFu, hasn[i], nnext[i], enext[i] >> 16);
                 o += byte == 0xFFu ? 1u : 0u;
             }
-            if (segl[i] && (c != nch - 1 || g.more_after)) o += 2;  // RSTm (extension)
+            if (segl[i] && (c != nch - 1 || (g.more_after && g.restart_interval > 0))) o += 2;  // RSTm (extension)
             ob[i] = o;
             mine += o;
             run = e;
@@ -542,11 +555,12 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
     // bit offsets inside the restart segments: segmented scan of the chunk bits
     bool f = false;
     unsigned long long v = 0;
-    for (int c = c0; c < c1; ++c) seg_combine(f, v, chunk_span(g, c).seg_first, cbits[c]);
+    for (int c = c0; c < c1; ++c)
+        seg_combine(f, v, chunk_span(g, c).seg_first, cbits[c] + (c == 0 ? (unsigned long long)g.bit_phase : 0ull));
     unsigned long long run = block_segscan_1024(f, v, sWave, sWaveF);
     unsigned long long mine = 0;
     for (int c = c0; c < c1; ++c) {
-        if (chunk_span(g, c).seg_first) run = 0;
+        if (chunk_span(g, c).seg_first) run = c == 0 ? (unsigned long long)g.bit_phase : 0ull;
         bit0[c] = run;
         mine += chunk_out_bytes(cff, cbits, cedge, g, c, run);
         run += cbits[c];
@@ -594,11 +608,13 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
             base[total_out[frame]] = 0xFF;
             base[total_out[frame] + 1] = 0xD9;
             out_len[frame] = (uint32_t)(end + 2);
-        } else if (sp.seg_last) {  // RSTm closing restart segment m (extension; not stuffed)
+        } else if (sp.seg_last && g.restart_interval > 0) {  // RSTm closing restart segment m (extension; not stuffed)
             const unsigned long long at = (last ? total_out[frame] : chunk_out[cid + 1]) - 2;
             base[at] = 0xFF;
             base[at + 1] = (uint8_t)(0xD0 + ((g.seg_base + sp.seg) & 7));
             if (last) out_len[frame] = (uint32_t)end;  // a stripe that more stripes follow
+        } else if (last) {
+            out_len[frame] = (uint32_t)end;  // a joined stripe that more stripes follow
         }
     }
     const unsigned long long b0 = chunk_bit0[cid];
@@ -611,9 +627,11 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
     const bool shared_tail = (e & 7) != 0;
     uint32_t tail = 0;
     if (shared_tail) {
-        const bool has_next = !sp.seg_last;
-        tail = boundary_byte((int)(e & 7), chunk_edge[cid] & 0xFFFFu, has_next, has_next ? chunk_bits[cid + 1] : 0u,
-                             has_next ? chunk_edge[cid + 1] >> 16 : 0u);
+        const bool jt = joined_tail(g, c);
+        const bool has_next = !sp.seg_last || jt;
+        tail = boundary_byte((int)(e & 7), chunk_edge[cid] & 0xFFFFu, has_next,
+                             jt ? (uint32_t)g.next_bits : (has_next ? chunk_bits[cid + 1] : 0u),
+                             jt ? g.next16 : (has_next ? chunk_edge[cid + 1] >> 16 : 0u));
     }
     const uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
     const unsigned off = (unsigned)(8 * kbeg - b0);  // the first owned byte starts this many bits into the chunk

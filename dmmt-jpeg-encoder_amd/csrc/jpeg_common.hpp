@@ -43,7 +43,12 @@ struct Geom {
     int sof_height;         // image height written into SOF
     int seg_base;           // global index of the first restart segment (RSTm numbering)
     int stripe_first;       // the stripe starts the image: write the header
-    int more_after;         // more stripes follow: close with RSTm instead of EOI
+    int more_after;         // more stripes follow: close with RSTm (restart mode) instead of EOI
+    // joined stripes (no restart intervals, reference-exact): the stripe's scan
+    // continues the previous stripe's mid-byte and runs on into the next one
+    int bit_phase;          // global scan bit offset of the stripe's first bit, mod 8
+    int next_bits;          // bits of the scan after the stripe known here (0..16)
+    uint32_t next16;        // those bits, MSB-aligned in 16
 };
 
 inline Geom make_geom(int width, int height, int subsampling, int maxval, int restart_interval) {
@@ -74,6 +79,9 @@ inline Geom make_geom(int width, int height, int subsampling, int maxval, int re
     g.seg_base = 0;
     g.stripe_first = 1;
     g.more_after = 0;
+    g.bit_phase = 0;
+    g.next_bits = 0;
+    g.next16 = 0;
     return g;
 }
 

@@ -111,6 +111,12 @@ def lib():
     L.dmmt_stripe_encode.argtypes = [vp, H, vp, sz, P(ctypes.c_uint64)]
     L.dmmt_stripe_max_bytes.argtypes = [P(DmmtStripe), P(DmmtOptions)]
     L.dmmt_stripe_max_bytes.restype = sz
+    I3 = ctypes.c_int16 * 3
+    L.dmmt_stripe_dc_edges.argtypes = [vp, I3, I3]
+    L.dmmt_stripe_fix_dc_hist.argtypes = [H, I3, I3]
+    L.dmmt_stripe_fix_dc_hist.restype = None
+    L.dmmt_stripe_measure.argtypes = [vp, H, I3, vp, sz, P(ctypes.c_uint64), P(ctypes.c_uint32)]
+    L.dmmt_stripe_write.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_uint64)]
     L.dmmt_build_info.argtypes = []
     L.dmmt_build_info.restype = ctypes.c_char_p
     _lib = L
@@ -435,6 +441,35 @@ class Encoder:
         _check(lib().dmmt_stripe_encode(self._ctx, h, d_out, out_cap, ctypes.byref(n)), "stripe_encode")
         return int(n.value)
 
+    # joined stripes (restart_interval 0, the reference's own stream)
+    def stripe_dc_edges(self):
+        """(first DC, last DC) per component (Y, Cb, Cr) of the analysed stripe"""
+        f, l = (ctypes.c_int16 * 3)(), (ctypes.c_int16 * 3)()
+        _check(lib().dmmt_stripe_dc_edges(self._ctx, f, l), "stripe_dc_edges")
+        return list(f), list(l)
+
+    @staticmethod
+    def stripe_fix_dc_hist(hist, first_dc, prev_last_dc) -> np.ndarray:
+        """the stripe's histograms with its first DC differences taken from the previous
+        stripe's last DCs instead of 0"""
+        h = (ctypes.c_uint64 * STRIPE_HIST_WORDS)(*[int(x) for x in hist])
+        lib().dmmt_stripe_fix_dc_hist(h, (ctypes.c_int16 * 3)(*first_dc), (ctypes.c_int16 * 3)(*prev_last_dc))
+        return np.ctypeslib.as_array(h).copy()
+
+    def stripe_measure(self, hist_sum, prev_last_dc, d_out: int, out_cap: int):
+        """tables from the summed histograms and the stripe's bits; returns (bit count, first 16 bits)"""
+        h = (ctypes.c_uint64 * STRIPE_HIST_WORDS)(*[int(x) for x in hist_sum])
+        bits, f16 = ctypes.c_uint64(), ctypes.c_uint32()
+        _check(lib().dmmt_stripe_measure(self._ctx, h, (ctypes.c_int16 * 3)(*prev_last_dc), d_out, out_cap,
+                                         ctypes.byref(bits), ctypes.byref(f16)), "stripe_measure")
+        return int(bits.value), int(f16.value)
+
+    def stripe_write(self, bit_offset: int, next_bits: int, next16: int) -> int:
+        """the stripe's stuffed bytes (after the header, for the first stripe); returns their count"""
+        n = ctypes.c_uint64()
+        _check(lib().dmmt_stripe_write(self._ctx, bit_offset, next_bits, next16, ctypes.byref(n)), "stripe_write")
+        return int(n.value)
+
     def set_profiling(self, on: bool):
         _check(lib().dmmt_ctx_set_profiling(self._ctx, 1 if on else 0))
 
@@ -456,21 +491,59 @@ def stripe_rows(mcuy: int, world: int, rank: int, rows_per_interval: int = 1):
     return row0, min(hi * rows_per_interval, mcuy) - row0
 
 
+def stripe_seam(bits, first16, k: int):
+    """(B_k, next_bits, next16) of stripe k from every stripe's (bit count, first 16
+    bits): its global scan bit offset and the up to 16 scan bits that follow it"""
+    b_k = int(sum(bits[:k]))
+    have, nxt = 0, 0
+    for j in range(k + 1, len(bits)):
+        t = min(16 - have, int(bits[j]), 16)
+        if t > 0:
+            nxt |= ((int(first16[j]) >> (16 - t)) << (16 - have - t))
+            have += t
+        if have == 16:
+            break
+    return b_k, have, nxt
+
+
 def encode_striped(enc: "Encoder", stripe: DmmtStripe, options: JpegTransformationOptions, d_out: int,
                    out_cap: int, group=None):
     """One image over the ranks of a torch.distributed group, one MCU-row stripe per
-    rank: the only exchange is an all-reduce of the 544 histogram
-    counters (the Huffman tables are global per image) and an all-gather of the
-    stripe sizes.  Returns (bytes of this stripe in d_out, its offset in the file,
-    file size); the stripes concatenated in rank order are the JPEG file."""
+    rank.  With restart intervals the stripes are independent restart
+    segments: the only exchange is an all-reduce of the 544 histogram counters (the
+    Huffman tables are global per image) and an all-gather of the stripe sizes.
+    Without (restart_interval 0, the reference's own stream) two small all-gathers
+    join the seams: the stripes' edge DCs before the all-reduce (the DC predictor runs
+    on across a seam) and their (bit count, first 16 bits) before the bytes are
+    written (stripe k starts at bit B_k, mid-byte).  Returns (bytes of this stripe in
+    d_out, its offset in the file, file size); the stripes concatenated in rank order
+    are the JPEG file."""
     import torch
     import torch.distributed as dist
     hist = enc.stripe_analyze(stripe, options)
     on_gpu = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+
+    def gather(vals):
+        out = torch.zeros(world * len(vals), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, torch.tensor(vals, dtype=torch.int64, device=dev), group=group)
+        return out.cpu().view(world, len(vals)).tolist()
+
+    joined = options.restart_interval == 0
+    if joined:  # the DC predictors run on across the seams: exchange the edge DCs first
+        first, last = enc.stripe_dc_edges()
+        edges = gather(first + last)
+        prev = edges[rank - 1][3:] if rank > 0 else [0, 0, 0]
+        hist = Encoder.stripe_fix_dc_hist(hist, first, prev)
     t = torch.from_numpy(hist.astype(np.int64)).to(dev)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    n = enc.stripe_encode(t.cpu().numpy().astype(np.uint64), d_out, out_cap)
+    if joined:  # the scan runs on across the seams: exchange the stripes' bit counts and heads
+        bits, f16 = enc.stripe_measure(t.cpu().numpy().astype(np.uint64), prev, d_out, out_cap)
+        seams = gather([bits, f16])
+        n = enc.stripe_write(*stripe_seam([b for b, _ in seams], [f for _, f in seams], rank))
+    else:
+        n = enc.stripe_encode(t.cpu().numpy().astype(np.uint64), d_out, out_cap)
     sizes = torch.zeros(dist.get_world_size(group), dtype=torch.int64, device=dev)
     mine = torch.tensor([n], dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(sizes, mine, group=group)
@@ -566,6 +639,6 @@ __all__ = [
     "Error", "LibraryMissing", "build", "lib", "ChromaSubsamplingPreset", "QuantizationTablePreset",
     "JpegTransformationOptions", "Image", "PPMImageReader", "Encoder", "JpegImageWriter", "Arguments",
     "convert_ppm_to_jpeg", "quantization_preset", "quality_tables", "max_jpeg_bytes", "device_count",
-    "DmmtStripe", "stripe_rows", "encode_striped",
+    "DmmtStripe", "stripe_rows", "stripe_seam", "encode_striped",
     "AraiDiscrete8x8CosineTransformer", "encode_array", "io",
 ]

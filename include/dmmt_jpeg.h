@@ -146,7 +146,8 @@ size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t subsampling)
  *                        the first stripe, its restart segments, then RSTm (more stripes
  *                        follow) or EOI (the image ends)
  * The stripes' outputs concatenated in row order are byte-identical to dmmt_jpeg_encode of
- * the whole image with the same restart interval. */
+ * the whole image with the same restart interval.  Without restart intervals see
+ * "joined stripes" below. */
 typedef struct dmmt_stripe {
     const void* d_rgb;          /* device: the stripe's pixel rows only, interleaved R,G,B */
     uint16_t width, height;     /* the whole image */
@@ -160,6 +161,33 @@ int dmmt_stripe_analyze(dmmt_ctx* ctx, const dmmt_stripe* stripe, const dmmt_opt
 int dmmt_stripe_encode(dmmt_ctx* ctx, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS], uint8_t* d_out,
                        size_t out_cap, uint64_t* out_len);
 size_t dmmt_stripe_max_bytes(const dmmt_stripe* stripe, const dmmt_options* opt);
+
+/* Joined stripes: restart_interval 0, the reference's own stream (SURVEY.md 8(e)
+ * "reference-exact mode").  Any MCU-row split works; stripe k's scan starts at
+ * global bit B_k = bits of stripes 0..k-1, usually mid-byte.  Protocol:
+ *   dmmt_stripe_analyze      as above; the stripe's first block per component is
+ *                            counted with predictor 0
+ *   dmmt_stripe_dc_edges     its first and last DC per component (Y, Cb, Cr)
+ *   (exchange 1)             all-gather of the edges; rank k > 0 applies
+ *   dmmt_stripe_fix_dc_hist  with stripe k-1's last DCs (categorize.rs:153-169
+ *                            across the seam), then the histogram sum
+ *   dmmt_stripe_measure      tables, the stripe's bits: its length and first 16 bits;
+ *                            the first stripe's JFIF header goes into d_out
+ *   (exchange 2)             all-gather of (bits, first16): B_k and the 16 bits of
+ *                            the scan after stripe k (fewer where the scan ends)
+ *   dmmt_stripe_write        the bytes whose first bit lies in the stripe (the byte
+ *                            it shares with the next stripe included), stuffed; EOI
+ *                            after the last stripe
+ * The outputs concatenated in row order are byte-identical to dmmt_jpeg_encode of the
+ * whole image (encoder.rs:125-135, 264-282). */
+int dmmt_stripe_dc_edges(dmmt_ctx* ctx, int16_t first_dc[3], int16_t last_dc[3]);
+void dmmt_stripe_fix_dc_hist(uint64_t hist[DMMT_STRIPE_HIST_WORDS], const int16_t first_dc[3],
+                             const int16_t prev_last_dc[3]);
+/* prev_last_dc: stripe k-1's last DCs (zeros for the first stripe); d_out as dmmt_stripe_encode */
+int dmmt_stripe_measure(dmmt_ctx* ctx, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS], const int16_t prev_last_dc[3],
+                        uint8_t* d_out, size_t out_cap, uint64_t* bits, uint32_t* first16);
+/* bit_offset: B_k; next16: the next_bits (<= 16) scan bits after the stripe, MSB-aligned */
+int dmmt_stripe_write(dmmt_ctx* ctx, uint64_t bit_offset, uint32_t next_bits, uint32_t next16, uint64_t* out_len);
 
 /* ---- stage-level entry points (parity tests) ---------------------------------------- */
 /* Front half only (transformer.rs:188-199): quantised zigzag blocks, MCU emission order

@@ -127,3 +127,43 @@ def test_product_does_not_reference_the_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h", "Makefile")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "cpu_ref" not in src and "import oracle" not in src and "libcpu_ref" not in src, f
+
+
+def _category(v):
+    return int(abs(int(v))).bit_length()
+
+
+def test_stripe_fix_dc_hist(L):
+    """joined stripes: a stripe's first DC difference per component, counted from
+    predictor 0 by the stripe, moves to the category of (first - previous stripe's
+    last), as i16 (categorize.rs:153-169)"""
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        hist = rng.integers(1, 1000, dmmt_jpeg.STRIPE_HIST_WORDS).astype(np.uint64)
+        first = [int(x) for x in rng.integers(-1024, 1024, 3)]
+        prev = [int(x) for x in rng.integers(-1024, 1024, 3)]
+        out = dmmt_jpeg.Encoder.stripe_fix_dc_hist(hist, first, prev)
+        want = hist.copy()
+        for i, base in enumerate((0, 272, 272)):
+            want[base + _category(first[i])] -= 1
+            d = ((first[i] - prev[i] + 32768) % 65536) - 32768
+            want[base + _category(d)] += 1
+        assert np.array_equal(out, want)
+
+
+def test_stripe_seam_composition():
+    """(B_k, next_bits, next16) equal a slice of the concatenated stripe bit strings,
+    including stripes shorter than 16 bits and the end of the scan"""
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        n = int(rng.integers(1, 9))
+        lens = [int(x) for x in rng.integers(0, 40, n)]
+        strs = ["".join(rng.choice(["0", "1"], size=m)) for m in lens]
+        f16 = [int((s[:16] + "0" * 16)[:16], 2) for s in strs]
+        whole = "".join(strs)
+        for k in range(n):
+            b, nb, nx = dmmt_jpeg.stripe_seam(lens, f16, k)
+            assert b == sum(lens[:k])
+            tail = whole[b + lens[k]:b + lens[k] + 16]
+            assert nb == len(tail)
+            assert nx == (int((tail + "0" * 16)[:16], 2) if tail else 0)

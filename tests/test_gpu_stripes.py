@@ -1,7 +1,9 @@
-"""One image over several GPUs as MCU-row stripes (BASELINE config 4's structure):
-dmmt_stripe_analyze -> histogram sum (the one exchange) -> dmmt_stripe_encode.
-The stripes concatenated must equal, byte for byte, the single encode of the whole
-image with the same restart interval (and so the oracle's)."""
+"""One image over several GPUs as MCU-row stripes (BASELINE config 4's structure).
+Restart mode: dmmt_stripe_analyze -> histogram sum (the one exchange) ->
+dmmt_stripe_encode.  Joined mode (no restart intervals, the reference's own stream):
+analyze -> edge-DC exchange + histogram sum -> measure -> (bits, head) exchange ->
+write.  The stripes concatenated must equal, byte for byte, the single encode of the
+whole image with the same options (and so the oracle's)."""
 import json
 import os
 import socket
@@ -59,6 +61,93 @@ def _striped_on_one_gpu(rgb, sub, q, rows_per_interval, n_stripes):
     return b"".join(parts), opts
 
 
+def _joined_on_one_gpu(rgb, sub, q, n_stripes):
+    """the joined-stripe protocol with one context per stripe, the exchanges done here"""
+    h, w, _ = rgb.shape
+    mcuy = -(-h // MCU_H[sub])
+    opts = _opts(sub, q, 0)
+    encs = [dmmt_jpeg.Encoder(0) for _ in range(n_stripes)]
+    bufs, heads = [], []
+    try:
+        hists, edges = [], []
+        for r, enc in enumerate(encs):
+            row0, rows = dmmt_jpeg.stripe_rows(mcuy, n_stripes, r)
+            y0, y1 = row0 * MCU_H[sub], min((row0 + rows) * MCU_H[sub], h)
+            px = np.ascontiguousarray(rgb[y0:y1])
+            d_in = enc.malloc(px.nbytes)
+            enc.h2d(d_in, px)
+            st = enc.stripe(d_in, w, h, row0, rows)
+            cap = enc.stripe_max_bytes(st, opts)
+            d_out = enc.malloc(cap)
+            bufs.append((enc, d_in, d_out, cap))
+            hists.append(enc.stripe_analyze(st, opts))
+            edges.append(enc.stripe_dc_edges())
+        prevs = [[0, 0, 0]] + [edges[r - 1][1] for r in range(1, n_stripes)]
+        total = np.zeros(dmmt_jpeg.STRIPE_HIST_WORDS, np.uint64)
+        for r in range(n_stripes):  # exchange 1: edge DCs, then the sum
+            total += dmmt_jpeg.Encoder.stripe_fix_dc_hist(hists[r], edges[r][0], prevs[r]) if r else hists[r]
+        for r, (enc, d_in, d_out, cap) in enumerate(bufs):
+            heads.append(enc.stripe_measure(total, prevs[r], d_out, cap))
+        bits, f16 = [b for b, _ in heads], [f for _, f in heads]
+        parts = []
+        for r, (enc, d_in, d_out, cap) in enumerate(bufs):  # exchange 2: bit counts and heads
+            n = enc.stripe_write(*dmmt_jpeg.stripe_seam(bits, f16, r))
+            parts.append(enc.d2h(d_out, n))
+    finally:
+        for (enc, d_in, d_out, cap) in bufs:
+            enc.free(d_in)
+            enc.free(d_out)
+        for enc in encs:
+            enc.close()
+    return b"".join(parts), opts
+
+
+@pytest.mark.parametrize("sub", [0, 1, 2])
+@pytest.mark.parametrize("shape,n_stripes", [((120, 200), 3), ((37, 53), 2), ((256, 96), 7), ((64, 64), 1),
+                                             ((129, 31), 5)])
+def test_joined_stripes_equal_reference_stream(encoder, sub, shape, n_stripes):
+    h, w = shape
+    rgb = synthetic(w, h, frame=h + 1)
+    data, opts = _joined_on_one_gpu(rgb, sub, 75, n_stripes)
+    assert data == encoder.encode(dmmt_jpeg.Image.from_array(rgb), opts)
+    assert data == oracle.encode(rgb, 255, sub, opts.luma_table, opts.chroma_table)
+
+
+@pytest.mark.parametrize("sub", [0, 2])
+def test_joined_stripes_shorter_than_a_byte(encoder, sub):
+    """a flat image: one-MCU stripes of a few bits each, so seams fall inside bytes
+    shared by three or more stripes and the 0xFF 1-padding spans stripes"""
+    w, h = MCU_W[sub], 8 * MCU_H[sub]
+    rgb = np.full((h, w, 3), 97, np.uint8)
+    data, opts = _joined_on_one_gpu(rgb, sub, 50, 8)
+    assert data == oracle.encode(rgb, 255, sub, opts.luma_table, opts.chroma_table)
+    rgb[::3] = 255  # 0xFF-rich rows
+    data, opts = _joined_on_one_gpu(rgb, sub, 50, 8)
+    assert data == oracle.encode(rgb, 255, sub, opts.luma_table, opts.chroma_table)
+
+
+def test_joined_stripes_4k_8way(encoder):
+    rgb = synthetic(3840, 2160, frame=12)
+    data, opts = _joined_on_one_gpu(rgb, 0, 90, 8)
+    assert data == oracle.encode(rgb, 255, 0, opts.luma_table, opts.chroma_table, threads=8)
+
+
+def test_joined_protocol_order_enforced(encoder):
+    d = encoder.malloc(64 * 16 * 3)
+    try:
+        with pytest.raises(dmmt_jpeg.Error):  # nothing analysed
+            encoder.stripe_write(0, 0, 0)
+        opts = _opts(0, 75, 0)
+        st = encoder.stripe(d, 64, 16, 1, 1)
+        encoder.stripe_analyze(st, opts)
+        with pytest.raises(dmmt_jpeg.Error):  # joined stripes are written by measure + write
+            encoder.stripe_encode(np.zeros(dmmt_jpeg.STRIPE_HIST_WORDS, np.uint64), d, 1 << 20)
+        with pytest.raises(dmmt_jpeg.Error):  # measure first
+            encoder.stripe_write(0, 0, 0)
+    finally:
+        encoder.free(d)
+
+
 @pytest.mark.parametrize("sub", [0, 1, 2])
 @pytest.mark.parametrize("shape,n_stripes,rpi", [((120, 200), 3, 1), ((37, 53), 2, 1), ((256, 96), 4, 2),
                                                   ((64, 64), 1, 1)])
@@ -87,13 +176,14 @@ def test_stripe_must_align_to_restart_intervals(encoder):
         with pytest.raises(dmmt_jpeg.Error) as e:
             encoder.stripe_analyze(st, opts)
         assert e.value.code == -102
-        with pytest.raises(dmmt_jpeg.Error):  # no restart interval: stripes are not independent
-            encoder.stripe_analyze(encoder.stripe(d, 64, 16, 0, 1), _opts(0, 75, 0))
+        with pytest.raises(dmmt_jpeg.Error):  # a restart-mode stripe has no joined seams
+            encoder.stripe_analyze(encoder.stripe(d, 64, 16, 0, 1), _opts(0, 75, 8))
+            encoder.stripe_dc_edges()
     finally:
         encoder.free(d)
 
 
-def _rank(rank, world, port, out_dir):
+def _rank(rank, world, port, out_dir, joined):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "dmmt-jpeg-encoder_amd"))
@@ -108,7 +198,7 @@ def _rank(rank, world, port, out_dir):
     y0, y1 = row0 * 16, min((row0 + rows) * 16, h)
     d_in = enc.malloc(w * (y1 - y0) * 3)
     enc.fill_synthetic_rows(d_in, w, h, y0, y1 - y0, frame=5)
-    opts = _opts(sub, 75, mcux)
+    opts = _opts(sub, 75, 0 if joined else mcux)
     st = enc.stripe(d_in, w, h, row0, rows)
     cap = enc.stripe_max_bytes(st, opts)
     d_out = enc.malloc(cap)
@@ -124,17 +214,18 @@ def _rank(rank, world, port, out_dir):
 
 
 @pytest.mark.timeout(300)
-def test_stripes_two_processes_gloo(tmp_path):
+@pytest.mark.parametrize("joined", [False, True])
+def test_stripes_two_processes_gloo(tmp_path, joined):
     """The multi-rank protocol for real: two processes (one context each, both on
-    GPU 0 here), the histogram all-reduce and size all-gather over gloo."""
+    GPU 0 here), the exchanges over gloo."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.start_processes(_rank, args=(2, port, str(tmp_path)), nprocs=2, start_method="spawn")
+    mp.start_processes(_rank, args=(2, port, str(tmp_path), joined), nprocs=2, start_method="spawn")
     metas = [json.load(open(tmp_path / f"meta{r}.json")) for r in range(2)]
     data = b"".join(open(tmp_path / f"part{r}.bin", "rb").read() for r in range(2))
     assert metas[1]["off"] == metas[0]["n"] and metas[0]["total"] == len(data)
     rgb = synthetic(320, 176, frame=5)
-    opts = _opts(2, 75, 320 // 16)
+    opts = _opts(2, 75, 0 if joined else 320 // 16)
     assert data == oracle.encode(rgb, 255, 2, opts.luma_table, opts.chroma_table,
                                  restart_interval=opts.restart_interval)
