@@ -51,7 +51,7 @@ struct dmmt_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace (grown on demand, never shrunk)
-    DevBuf coef, dc, dcdiff, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff, chunk_edge,
+    DevBuf coef, dc, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff, chunk_edge,
         chunk_bit0, chunk_out, status, lut, qtab, qtab_u8;
     // host-API staging
     DevBuf in, out, out_len, dct;
@@ -175,6 +175,7 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     if ((rc = ensure(c->coef, nb * 64 * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dc, nb * sizeof(int16_t)))) return rc;
     if ((rc = ensure(c->dcdiff, nb * sizeof(int16_t)))) return rc;
+    if ((rc = ensure(c->lastnz, nb))) return rc;
     // staging slots sized for the worst case; k_stuffwrite reads up to 4 words
     // past a slot's last bit, hence the tail
     if ((rc = ensure(c->stage, (nch * (size_t)kChunkWordsCap + 64) * sizeof(uint32_t)))) return rc;
@@ -194,6 +195,7 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
     w->coef = (int16_t*)c->coef.p;
     w->dc = (int16_t*)c->dc.p;
     w->dcdiff = (int16_t*)c->dcdiff.p;
+    w->lastnz = (uint8_t*)c->lastnz.p;
     w->ac_hist = (uint32_t*)c->ac_hist.p;
     w->dc_hist = (uint32_t*)c->dc_hist.p;
     w->code_tab = (uint32_t*)c->code_tab.p;

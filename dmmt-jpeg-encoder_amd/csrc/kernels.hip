@@ -177,11 +177,12 @@ struct RawTile {
 //  D  coalesced 16-byte stores of the tile's blocks + DC values (wave 3), beside
 //  E  AC symbols (waves 0-2): two threads per block walk its coefficients from
 //     registers; LDS histogram, flushed once per workgroup.
-template <int HR, int VR, typename Sample>
-__global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, size_t frame_stride, Geom g,
+template <int HR, int VR, typename Sample, int WPE>
+__global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ rgb, size_t frame_stride, Geom g,
                                                const float* __restrict__ norm_lut,
                                                const float* __restrict__ qtab,  // [2][64] natural, as f32
                                                int16_t* __restrict__ coef, int16_t* __restrict__ dc,
+                                               uint8_t* __restrict__ lastnz,
                                                uint32_t* __restrict__ ac_hist,  // [frames][reps][2][256]
                                                int* __restrict__ status) {
     constexpr int TM = 32 / HR;      // MCUs per tile
@@ -461,7 +462,10 @@ __global__ __launch_bounds__(256) void k_front(const Sample* __restrict__ rgb, s
                     ++run;
                 }
             }
-            if (half && run) atomicAdd(&h[0], 1u);  // EOB
+            if (half) {
+                if (run) atomicAdd(&h[0], 1u);                 // EOB
+                lastnz[e0 + blk] = (uint8_t)(63 - run);  // k_emit groups its walks by this
+            }
         }
         __syncthreads();
         DMMT_TRACE(4);
@@ -899,12 +903,6 @@ __global__ __launch_bounds__(256) void k_synthetic(uint8_t* __restrict__ rgb, in
 }
 
 // explicit instantiations of the front kernel
-template __global__ void k_front<1, 1, uint8_t>(const uint8_t*, size_t, Geom, const float*, const float*, int16_t*, int16_t*, uint32_t*, int*);
-template __global__ void k_front<2, 1, uint8_t>(const uint8_t*, size_t, Geom, const float*, const float*, int16_t*, int16_t*, uint32_t*, int*);
-template __global__ void k_front<2, 2, uint8_t>(const uint8_t*, size_t, Geom, const float*, const float*, int16_t*, int16_t*, uint32_t*, int*);
-template __global__ void k_front<1, 1, uint16_t>(const uint16_t*, size_t, Geom, const float*, const float*, int16_t*, int16_t*, uint32_t*, int*);
-template __global__ void k_front<2, 1, uint16_t>(const uint16_t*, size_t, Geom, const float*, const float*, int16_t*, int16_t*, uint32_t*, int*);
-template __global__ void k_front<2, 2, uint16_t>(const uint16_t*, size_t, Geom, const float*, const float*, int16_t*, int16_t*, uint32_t*, int*);
 
 }  // namespace dmmt
 
@@ -913,7 +911,7 @@ template __global__ void k_front<2, 2, uint16_t>(const uint16_t*, size_t, Geom, 
 // DC values and AC histograms k_front would have produced are rebuilt here.
 namespace dmmt {
 __global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coef, Geom g, int16_t* __restrict__ dc,
-                                                 uint32_t* __restrict__ ac_hist) {
+                                                 uint8_t* __restrict__ lastnz, uint32_t* __restrict__ ac_hist) {
     __shared__ uint32_t sHist[512];
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
@@ -922,8 +920,11 @@ __global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coe
     const long long base = (long long)frame * g.bpf;
     for (long long el = (long long)blockIdx.x * 4 + wave; el < g.bpf; el += (long long)gridDim.x * 4) {
         const int c = coef[(base + el) * 64 + lane];
-        if (lane == 0) dc[base + el] = (int16_t)c;
         const unsigned long long nz = __ballot(c != 0) & ~1ull;
+        if (lane == 0) {
+            dc[base + el] = (int16_t)c;
+            lastnz[base + el] = (uint8_t)(nz ? 63 - __clzll(nz) : 0);
+        }
         const int t = (int)(el % g.bpm) < g.n_luma ? 0 : 1;
         if (lane > 0 && c != 0) {
             const unsigned long long below = nz & ((1ull << lane) - 1ull);
@@ -944,7 +945,19 @@ __global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coe
 // ============================================================== launchers
 namespace dmmt {
 
+#ifndef FRONT_WPE_420
+#define FRONT_WPE_420 1
+#endif
+
 static inline int clampi(long long v, int lo, int hi) { return (int)(v < lo ? lo : (v > hi ? hi : v)); }
+
+// Waves per SIMD k_front is compiled for (register budget 512 / WPE): u8 4:4:4
+// and 4:2:2 fit 128 registers, four resident workgroups per CU; the rest keep the
+// allocation the compiler picks.
+template <int HR, int VR, typename S>
+constexpr int front_wpe() {
+    return sizeof(S) == 1 ? (HR * VR == 4 ? FRONT_WPE_420 : 4) : 1;
+}
 
 template <int HR, int VR, typename S>
 static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const Geom& g, const Work& w,
@@ -955,7 +968,7 @@ static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const
     static int resident = 0;
     if (!resident) {
         int per_cu = 0, dev = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_front<HR, VR, S>, 256, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_front<HR, VR, S, front_wpe<HR, VR, S>()>, 256, 0) != hipSuccess ||
             per_cu < 1)
             per_cu = 2;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -965,8 +978,8 @@ static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const
         resident = per_cu * cus;
     }
     dim3 grid(clampi(ntiles, 1, resident / n_frames > 0 ? resident / n_frames : 1), n_frames);
-    hipLaunchKernelGGL((k_front<HR, VR, S>), grid, dim3(256), 0, st, (const S*)rgb, stride_elems, g, w.norm_lut,
-                       w.qtab, w.coef, w.dc, w.ac_hist, w.status);
+    hipLaunchKernelGGL((k_front<HR, VR, S, front_wpe<HR, VR, S>()>), grid, dim3(256), 0, st, (const S*)rgb, stride_elems, g, w.norm_lut,
+                       w.qtab, w.coef, w.dc, w.lastnz, w.ac_hist, w.status);
 }
 
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
@@ -999,7 +1012,7 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 
 hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
     dim3 grid(clampi((g.bpf + 3) / 4, 1, 1024 / n_frames > 0 ? 1024 / n_frames : 1), n_frames);
-    hipLaunchKernelGGL(k_ac_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, g, w.dc, w.ac_hist);
+    hipLaunchKernelGGL(k_ac_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, g, w.dc, w.lastnz, w.ac_hist);
     return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@ struct Work {
     int16_t* coef;                  // [frames][bpf][64] zigzag, emission order
     int16_t* dc;                    // [frames][bpf]
     int16_t* dcdiff;                // [frames][bpf]
+    uint8_t* lastnz;                // [frames][bpf] zigzag position of the last non-zero AC (0: none)
     uint32_t* ac_hist;              // [frames][reps][2][256], zero between launches
     uint32_t* dc_hist;              // [frames][reps][2][16], zero between launches
     uint32_t* code_tab;             // [frames][4][256]  (len << 16) | code
