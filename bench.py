@@ -181,6 +181,8 @@ def main(argv=None, make_encoder=None, emit=None):
     ap.add_argument("--config", default="4k444q90", choices=sorted(CONFIGS) + sorted(STRIPED))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--distinct-frames", type=int, default=4)
+    ap.add_argument("--lanes", type=int, default=4,
+                    help="pipeline lanes: consecutive steps overlap on this many workspaces/streams (1 = serial)")
     args = ap.parse_args(argv)
     make_encoder = make_encoder or dmmt_jpeg.Encoder
     emit = emit or (lambda line: print(line, flush=True))
@@ -216,45 +218,52 @@ def main(argv=None, make_encoder=None, emit=None):
     nslots = max(1, args.distinct_frames)
     frame_bytes = w * h * 3
     out_stride = (dmmt_jpeg.max_jpeg_bytes(w, h, sub) + 255) // 256 * 256
+    lanes = max(1, args.lanes)
     d_in = [enc.malloc(frame_bytes * fps) for _ in range(nslots)]
-    d_out = enc.malloc(out_stride * fps)
-    d_len = enc.malloc(4 * fps)
+    d_out = [enc.malloc(out_stride * fps) for _ in range(lanes)]  # one per lane: never shared by concurrent steps
+    d_len = [enc.malloc(4 * fps) for _ in range(lanes)]
     for s in range(nslots):  # distinct synthetic frames per slot and per rank
         enc.fill_synthetic(d_in[s], w, h, fps, first_frame=(rank * nslots + s) * fps)
 
-    def step(i):
-        enc.encode_device(d_in[i % nslots], fps, w, h, None, d_out, out_stride, d_len, frame_stride=frame_bytes,
-                          opt_c=opt_c)
+    def step(i, nl):
+        enc.encode_device(d_in[i % nslots], fps, w, h, None, d_out[i % nl], out_stride, d_len[i % nl],
+                          frame_stride=frame_bytes, opt_c=opt_c)
 
-    for i in range(args.warmup):
-        step(i)
-    barrier_sync(enc)
+    def timed(nl):
+        enc.set_lanes(nl)
+        for i in range(args.warmup):
+            step(i, nl)
+        barrier_sync(enc)
+        barrier_sync(enc)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i, nl)
+        barrier_sync(enc)
+        return time.perf_counter() - t0
 
-    # timed region: the production path (no event timing inside)
-    barrier_sync(enc)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    barrier_sync(enc)
-    elapsed = time.perf_counter() - t0
+    # timed region: the production path (no event timing inside); with lanes > 1
+    # consecutive frames are pipelined over the context's lanes (dmmt_ctx_set_lanes)
+    elapsed = timed(lanes)
+    # the same steps one at a time (one lane): the latency of one frame
+    single = timed(1) if lanes > 1 else elapsed
 
-    # roofline pass: the same steps again with HIP events around k_front on the
-    # stream it runs on
+    # roofline pass: the same steps again, one lane, with HIP events around k_front
+    # on the stream it runs on
     front = stage_index("front")
     enc.set_profiling(1 << front)
     barrier_sync(enc)
     for i in range(args.steps):
-        step(i)
+        step(i, 1)
     barrier_sync(enc)
     prof = enc.profile()
     enc.set_profiling(0)
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        t = torch.tensor([elapsed, single], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, single = (float(x) for x in t.tolist())
 
-    lens = np.frombuffer(enc.d2h(d_len, 4 * fps), np.uint32)
+    lens = np.frombuffer(enc.d2h(d_len[0], 4 * fps), np.uint32)
     jpeg_bytes = float(lens.mean())
 
     if rank == 0:
@@ -299,6 +308,9 @@ def main(argv=None, make_encoder=None, emit=None):
                             f"{fps} frame(s) per step per GPU, pixels in HBM -> JPEG files in HBM",
                 "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
                 "frames_per_step": fps, "mean_jpeg_bytes": jpeg_bytes, "parallelism": f"independent frames x{world}",
+                "lanes": lanes,
+                "single_lane_ms_per_step": round(single / args.steps * 1e3, 4),
+                "single_lane_value": round(pixels / single / 1e6, 2),
             },
             "roofline": {
                 "bound": "hbm",
@@ -316,7 +328,7 @@ def main(argv=None, make_encoder=None, emit=None):
             "cpu_baseline": cpu,
         }
         emit(json.dumps(line))
-    for p in d_in + [d_out, d_len]:
+    for p in d_in + d_out + d_len:
         enc.free(p)
     enc.close()
     if world > 1:

@@ -46,13 +46,24 @@ constexpr size_t kMaxGraphs = 16;
 
 }  // namespace
 
+// One pipeline lane: a device workspace (grown on demand, never shrunk) and the
+// stream that runs on it.  Lane 0 is the context's own stream; dmmt_ctx_set_lanes
+// adds lanes so that consecutive dmmt_encode_device calls overlap.
+struct Lane {
+    hipStream_t stream = nullptr;
+    DevBuf coef, dc, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
+        chunk_edge, chunk_bit0, chunk_out;
+};
+
 struct dmmt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    // workspace (grown on demand, never shrunk)
-    DevBuf coef, dc, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff, chunk_edge,
-        chunk_bit0, chunk_out, status, lut, qtab, qtab_u8;
+    std::vector<Lane*> lanes;  // lanes[0].stream == stream
+    int nlanes = 1;
+    unsigned next_lane = 0;
+    // shared by the lanes: status word (sticky error bits) and the uploaded tables
+    DevBuf status, lut, qtab, qtab_u8;
     // host-API staging
     DevBuf in, out, out_len, dct;
     // uploaded table state
@@ -132,6 +143,11 @@ int make_checked_geom(int w, int h, int sub, int maxval, int ri, Geom* g) {
     return DMMT_OK;
 }
 
+int sync_lanes(dmmt_ctx* c) {
+    for (Lane* L : c->lanes) HIP_TRY(hipStreamSynchronize(L->stream));
+    return DMMT_OK;
+}
+
 // Upload quantisation tables (f32 for the quantiser, u8 for DQT) and the
 // `v as f32 / max as f32` table (color.rs:45-53; host f32 division is IEEE
 // correctly rounded, identical to the reference's).
@@ -143,6 +159,7 @@ int upload_tables(dmmt_ctx* c, const dmmt_options* opt, int maxval, int sb, hipS
     memcpy(q, opt->luma_q, 64);
     memcpy(q + 64, opt->chroma_q, 64);
     if (!c->q_valid || memcmp(q, c->q_cached, 128) != 0) {
+        if ((rc = sync_lanes(c))) return rc;  // no lane may still read the old tables
         float qf[128];
         for (int i = 0; i < 128; ++i) qf[i] = (float)q[i];
         HIP_TRY(hipMemcpyAsync(c->qtab.p, qf, sizeof qf, hipMemcpyHostToDevice, st));
@@ -156,6 +173,7 @@ int upload_tables(dmmt_ctx* c, const dmmt_options* opt, int maxval, int sb, hipS
         return DMMT_OK;
     }
     if (c->lut_maxval != maxval || c->lut_sb != sb) {
+        if ((rc = sync_lanes(c))) return rc;
         const size_t n = sb == 1 ? 256 : 65536;
         if ((rc = ensure(c->lut, n * sizeof(float)))) return rc;
         std::vector<float> lut(n);
@@ -168,45 +186,46 @@ int upload_tables(dmmt_ctx* c, const dmmt_options* opt, int maxval, int sb, hipS
     return DMMT_OK;
 }
 
-int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
+int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane) {
     int rc;
+    Lane* L = c->lanes[lane];
     const size_t nb = (size_t)g.bpf * nf;
     const size_t nch = (size_t)g.nch * nf;
-    if ((rc = ensure(c->coef, nb * 64 * sizeof(int16_t)))) return rc;
-    if ((rc = ensure(c->dc, nb * sizeof(int16_t)))) return rc;
-    if ((rc = ensure(c->dcdiff, nb * sizeof(int16_t)))) return rc;
-    if ((rc = ensure(c->lastnz, nb))) return rc;
+    if ((rc = ensure(L->coef, nb * 64 * sizeof(int16_t)))) return rc;
+    if ((rc = ensure(L->dc, nb * sizeof(int16_t)))) return rc;
+    if ((rc = ensure(L->dcdiff, nb * sizeof(int16_t)))) return rc;
+    if ((rc = ensure(L->lastnz, nb))) return rc;
     // staging slots sized for the worst case; k_stuffwrite reads up to 4 words
     // past a slot's last bit, hence the tail
-    if ((rc = ensure(c->stage, (nch * (size_t)kChunkWordsCap + 64) * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c->chunk_bits, nch * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c->chunk_ff, nch * 8 * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c->chunk_edge, nch * sizeof(uint32_t)))) return rc;
-    if ((rc = ensure(c->chunk_bit0, nch * sizeof(unsigned long long)))) return rc;
-    if ((rc = ensure(c->chunk_out, nch * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(L->stage, (nch * (size_t)kChunkWordsCap + 64) * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(L->chunk_bits, nch * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(L->chunk_ff, nch * 8 * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(L->chunk_edge, nch * sizeof(uint32_t)))) return rc;
+    if ((rc = ensure(L->chunk_bit0, nch * sizeof(unsigned long long)))) return rc;
+    if ((rc = ensure(L->chunk_out, nch * sizeof(unsigned long long)))) return rc;
     // k_front / k_dcdiff add into the replicas, k_emit zeroes them after k_tables:
     // zero between launches, starting with the allocation
-    if ((rc = ensure(c->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
-    if ((rc = ensure(c->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
-    if ((rc = ensure(c->code_tab, (size_t)nf * 1024 * 4))) return rc;
-    if ((rc = ensure(c->hdr_len, (size_t)nf * 4))) return rc;
-    if ((rc = ensure(c->total_out, (size_t)nf * 8))) return rc;
+    if ((rc = ensure(L->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
+    if ((rc = ensure(L->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
+    if ((rc = ensure(L->code_tab, (size_t)nf * 1024 * 4))) return rc;
+    if ((rc = ensure(L->hdr_len, (size_t)nf * 4))) return rc;
+    if ((rc = ensure(L->total_out, (size_t)nf * 8))) return rc;
     if ((rc = ensure(c->status, 16, true))) return rc;
-    w->coef = (int16_t*)c->coef.p;
-    w->dc = (int16_t*)c->dc.p;
-    w->dcdiff = (int16_t*)c->dcdiff.p;
-    w->lastnz = (uint8_t*)c->lastnz.p;
-    w->ac_hist = (uint32_t*)c->ac_hist.p;
-    w->dc_hist = (uint32_t*)c->dc_hist.p;
-    w->code_tab = (uint32_t*)c->code_tab.p;
-    w->hdr_len = (uint32_t*)c->hdr_len.p;
-    w->stage = (uint32_t*)c->stage.p;
-    w->chunk_bits = (uint32_t*)c->chunk_bits.p;
-    w->chunk_ff = (uint32_t*)c->chunk_ff.p;
-    w->chunk_edge = (uint32_t*)c->chunk_edge.p;
-    w->chunk_bit0 = (unsigned long long*)c->chunk_bit0.p;
-    w->chunk_out = (unsigned long long*)c->chunk_out.p;
-    w->total_out = (unsigned long long*)c->total_out.p;
+    w->coef = (int16_t*)L->coef.p;
+    w->dc = (int16_t*)L->dc.p;
+    w->dcdiff = (int16_t*)L->dcdiff.p;
+    w->lastnz = (uint8_t*)L->lastnz.p;
+    w->ac_hist = (uint32_t*)L->ac_hist.p;
+    w->dc_hist = (uint32_t*)L->dc_hist.p;
+    w->code_tab = (uint32_t*)L->code_tab.p;
+    w->hdr_len = (uint32_t*)L->hdr_len.p;
+    w->stage = (uint32_t*)L->stage.p;
+    w->chunk_bits = (uint32_t*)L->chunk_bits.p;
+    w->chunk_ff = (uint32_t*)L->chunk_ff.p;
+    w->chunk_edge = (uint32_t*)L->chunk_edge.p;
+    w->chunk_bit0 = (unsigned long long*)L->chunk_bit0.p;
+    w->chunk_out = (unsigned long long*)L->chunk_out.p;
+    w->total_out = (unsigned long long*)L->total_out.p;
     w->status = (int*)c->status.p;
     w->norm_lut = nullptr;  // bound by prepare() after upload_tables
     w->qtab = nullptr;
@@ -215,9 +234,10 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w) {
 }
 
 // workspace + tables for one launch batch; every table pointer is valid on return
-int prepare(dmmt_ctx* c, const Geom& g, int nf, const dmmt_options* opt, int sb, hipStream_t st, Work* w) {
+int prepare(dmmt_ctx* c, const Geom& g, int nf, const dmmt_options* opt, int sb, hipStream_t st, Work* w,
+            int lane = 0) {
     int rc;
-    if ((rc = ensure_work(c, g, nf, w))) return rc;
+    if ((rc = ensure_work(c, g, nf, w, lane))) return rc;
     if ((rc = upload_tables(c, opt, g.maxval, sb, st))) return rc;
     w->norm_lut = (const float*)c->lut.p;
     w->qtab = (const float*)c->qtab.p;
@@ -319,10 +339,11 @@ void destroy_graphs(dmmt_ctx* c) {
 // one by one; replaying them as one instantiated graph removes most of that.
 // Stage profiling needs per-kernel events, so it always launches directly.
 int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, int nf, const Geom& g,
-                   const dmmt_options* opt, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st) {
+                   const dmmt_options* opt, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st,
+                   int lane = 0) {
     Work w;
     int rc;
-    if ((rc = prepare(c, g, nf, opt, sb, st, &w))) return rc;
+    if ((rc = prepare(c, g, nf, opt, sb, st, &w, lane))) return rc;
     const int bits = opt->bits_per_channel;
     if (!c->use_graphs || c->profile)
         return enqueue_direct(c, d_rgb, frame_stride, sb, nf, g, w, bits, out, out_stride, out_len, st);
@@ -384,6 +405,16 @@ int take_status(dmmt_ctx* c, hipStream_t st) {
 
 int set_device(dmmt_ctx* c) { return hip_err(hipSetDevice(c->device)); }
 
+void destroy_lane(Lane* L, bool own_stream) {
+    (void)hipStreamSynchronize(L->stream);
+    DevBuf* bufs[] = {&L->coef,     &L->dc,        &L->dcdiff,     &L->lastnz,     &L->ac_hist,
+                      &L->dc_hist,  &L->code_tab,  &L->hdr_len,    &L->total_out,  &L->stage,
+                      &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out};
+    for (DevBuf* b : bufs) release(*b);
+    if (own_stream) (void)hipStreamDestroy(L->stream);
+    delete L;
+}
+
 }  // namespace
 
 // ===================================================================== C ABI
@@ -412,6 +443,8 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
         delete c;
         return DMMT_E_HIP;
     }
+    c->lanes.push_back(new Lane());
+    c->lanes[0]->stream = c->stream;
     *out = c;
     return DMMT_OK;
 }
@@ -419,18 +452,39 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
 extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    (void)sync_lanes(c);
     drain_events(c);
     destroy_graphs(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
-    DevBuf* bufs[] = {&c->coef,       &c->dc,         &c->dcdiff,     &c->ac_hist,     &c->dc_hist,
-                      &c->code_tab,   &c->hdr_len,    &c->total_out,  &c->stage,
-                      &c->chunk_bits, &c->chunk_ff,   &c->chunk_edge, &c->chunk_bit0,  &c->chunk_out,
-                      &c->status,     &c->lut,        &c->qtab,       &c->qtab_u8,     &c->in,
-                      &c->out,        &c->out_len,    &c->dct};
+    for (size_t i = 0; i < c->lanes.size(); ++i) destroy_lane(c->lanes[i], i > 0);
+    DevBuf* bufs[] = {&c->status, &c->lut, &c->qtab, &c->qtab_u8, &c->in, &c->out, &c->out_len, &c->dct};
     for (DevBuf* b : bufs) release(*b);
     (void)hipStreamDestroy(c->stream);
     delete c;
+}
+
+extern "C" int dmmt_ctx_set_lanes(dmmt_ctx* c, int n) {
+    if (!c || n < 1 || n > DMMT_MAX_LANES) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    if ((rc = sync_lanes(c))) return rc;
+    while ((int)c->lanes.size() > n) {  // the workspaces of dropped lanes are freed
+        destroy_lane(c->lanes.back(), true);
+        c->lanes.pop_back();
+    }
+    while ((int)c->lanes.size() < n) {
+        Lane* L = new Lane();
+        if (hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete L;
+            return DMMT_E_HIP;
+        }
+        c->lanes.push_back(L);
+    }
+    destroy_graphs(c);
+    c->nlanes = n;
+    c->next_lane = 0;
+    return DMMT_OK;
 }
 
 extern "C" int dmmt_ctx_synchronize(dmmt_ctx* c) {
@@ -460,8 +514,13 @@ extern "C" int dmmt_encode_device(dmmt_ctx* c, const dmmt_device_frames* f, cons
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int lane = 0;
+    if (!stream && c->nlanes > 1) {  // pipelined: the next lane's workspace and stream
+        lane = (int)(c->next_lane++ % (unsigned)c->nlanes);
+        st = c->lanes[lane]->stream;
+    }
     return enqueue_encode(c, f->d_rgb, f->frame_stride, f->sample_bytes, f->n_frames, g, opt, f->d_out, f->out_stride,
-                          f->d_out_len, st);
+                          f->d_out_len, st, lane);
 }
 
 // Host-memory batch of equal-geometry images -> host JPEGs.

@@ -107,7 +107,7 @@ __device__ __forceinline__ int coef_at(const BlockCoef& b, int k) {
 
 template <typename Sink>
 __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const uint32_t* __restrict__ dctab,
-                                           const uint32_t* __restrict__ actab, Sink& sink) {
+                                           const uint32_t* __restrict__ actab, Sink& sink, int kmax = 63) {
     {
         const int cat = category_of(dcd);
         const uint32_t e = dctab[cat];
@@ -117,6 +117,7 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
     int run = 0;
 #pragma unroll
     for (int k = 1; k < 64; ++k) {
+        if (k > kmax) continue;  // (wave-uniform) every later position is zero in every lane
         const int v = coef_at(b, k);
         if (v != 0) {
             for (int r = run >> 4; r > 0; --r) sink(z & 0xFFFFu, (int)(z >> 16));
@@ -128,7 +129,7 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
             ++run;
         }
     }
-    if (run) {
+    if (run || kmax < 63) {
         const uint32_t e = actab[0];  // EOB
         sink(e & 0xFFFFu, (int)(e >> 16));
     }
@@ -224,6 +225,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     __shared__ uint32_t sBin[65];  // walk order: blocks counted, then started, by last non-zero position
     __shared__ uint8_t sOrder[256];  // block walked by thread u
+    __shared__ uint8_t sKey[256];    // its last non-zero position (ascending in u)
     __shared__ uint32_t sBits[256];  // bit count of block t
     DMMT_TRACE_START;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -260,7 +262,10 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     }
     __syncthreads();
     const int mine = valid ? (int)(sBin[key] + rank) : tid;
-    if (valid) sOrder[mine] = (uint8_t)tid;
+    if (valid) {
+        sOrder[mine] = (uint8_t)tid;
+        sKey[mine] = (uint8_t)key;
+    }
     __syncthreads();
     DMMT_TRACE(0);
     {
@@ -273,8 +278,10 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
             const int dp = dcdiff[ep];
             const int kp = ((int)(el0 % g.bpm) + p) % g.bpm;
             const uint32_t* tp = sTab + (kp < g.n_luma ? 0 : 512);
+            // the wave's walk stops after the last position any of its blocks uses
+            const int kmax = __builtin_amdgcn_readfirstlane((int)sKey[min(64 * wave + 63, nb - 1)]);
             SlotSink ss{sSlot + tid, 0ull, 0, 0};
-            walk_block(b, dp, tp, tp + 256, ss);
+            walk_block(b, dp, tp, tp + 256, ss, kmax);
             sBits[p] = ss.finish();
         }
     }

@@ -77,6 +77,7 @@ def lib():
     L.dmmt_jpeg_encode.argtypes = [vp, P(DmmtImage), P(DmmtOptions), P(vp), P(sz)]
     L.dmmt_jpeg_encode_batch.argtypes = [vp, P(DmmtImage), ctypes.c_int, P(DmmtOptions), P(vp), P(sz)]
     L.dmmt_encode_device.argtypes = [vp, P(DmmtDeviceFrames), P(DmmtOptions), vp]
+    L.dmmt_ctx_set_lanes.argtypes = [vp, ctypes.c_int]
     L.dmmt_max_jpeg_bytes.argtypes = [u16, u16, i32]
     L.dmmt_max_jpeg_bytes.restype = sz
     L.dmmt_forward_blocks.argtypes = [vp, P(DmmtImage), P(DmmtOptions), vp, sz, P(sz)]
@@ -388,6 +389,11 @@ class Encoder:
         f.d_out, f.out_stride, f.d_out_len = d_out, out_stride, d_out_len
         opt = opt_c if opt_c is not None else options.to_c()
         _check(lib().dmmt_encode_device(self._ctx, ctypes.byref(f), ctypes.byref(opt), stream), "encode_device")
+
+    def set_lanes(self, n: int):
+        """pipelined device encodes: consecutive encode_device calls with stream None
+        go round-robin to n workspaces and streams (include/dmmt_jpeg.h)"""
+        _check(lib().dmmt_ctx_set_lanes(self._ctx, n), "set_lanes")
 
     def synchronize(self):
         _check(lib().dmmt_ctx_synchronize(self._ctx), "synchronize")

@@ -133,6 +133,15 @@ int dmmt_jpeg_encode_batch(dmmt_ctx* ctx, const dmmt_image* imgs, int n, const d
 /* Device-resident form: frames in HBM -> JPEG files in HBM, enqueued on `stream`
  * (a hipStream_t, NULL = the context's stream), no host synchronisation. */
 int dmmt_encode_device(dmmt_ctx* ctx, const dmmt_device_frames* frames, const dmmt_options* opt, void* stream);
+/* Pipelined device encodes (extension of the above; the reference encodes one image at a
+ * time on the host): with n lanes (1..DMMT_MAX_LANES, default 1) a context keeps n
+ * workspaces and streams, and consecutive dmmt_encode_device calls with stream NULL go
+ * round-robin to them, so one call's latency-bound kernels (Huffman tables, offsets)
+ * overlap the next calls' kernels.  Calls with stream NULL then run concurrently: their
+ * inputs must be complete when the call is made, their outputs are complete after
+ * dmmt_ctx_synchronize.  A non-NULL stream always uses lane 0, in stream order. */
+#define DMMT_MAX_LANES 8
+int dmmt_ctx_set_lanes(dmmt_ctx* ctx, int n);
 size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t subsampling);
 
 /* ---- one image across several GPUs (extension) ---------------------------------------- */

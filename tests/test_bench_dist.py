@@ -47,6 +47,9 @@ class StandInEncoder:
     def synchronize(self):
         pass
 
+    def set_lanes(self, n):
+        self.log.append(("lanes", self.rank, n))
+
     def set_profiling(self, mask):
         self.mask = mask
 
@@ -88,8 +91,11 @@ def test_bench_two_ranks_gloo(tmp_path):
     line = json.loads(r0["lines"][0])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["steps"] == 20
     # distinct synthetic frames per rank (no two ranks encode the same frames)
-    f0 = {tuple(x[2:]) for x in r0["log"]}
-    f1 = {tuple(x[2:]) for x in r1["log"]}
+    f0 = {tuple(x[2:]) for x in r0["log"] if x[0] == "frames"}
+    f1 = {tuple(x[2:]) for x in r1["log"] if x[0] == "frames"}
+    # the timed steps run pipelined over the default lanes, then once serially
+    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 1]
+    assert line["config"]["lanes"] == 4 and line["config"]["single_lane_ms_per_step"] > 0
     assert f0 and f1 and not (f0 & f1)
     # elapsed is the MAX over ranks: at least the slow rank's sleeps
     assert line["ms_per_step"] >= STEP_SLEEP[1] * 1e3 * 0.9
