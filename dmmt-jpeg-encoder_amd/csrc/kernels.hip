@@ -69,6 +69,36 @@ __device__ __forceinline__ int16_t quantize_rcp(float d, float q, float rq) {
     return (int16_t)(int)x;
 }
 
+// quantize_rcp over the 8 rows of one column (row r scaled by q[8r], rq[8r] = 1/q):
+// branch-free on the fast path -- round half away from zero of a = |d * (1/q)| is
+// trunc(a + 0.5) there, exactly: a < 2^22 and a's fraction is farther than
+// a * 2^-20 > ulp(a + 0.5) / 2 from 1/2, so the addition cannot round across an
+// integer -- and the rare lanes outside it redone with the division afterwards.
+// out[i] packs rows 2i (low half) and 2i+1 (high half).
+__device__ __forceinline__ void quantize_col8(const float (&v)[8], const float* q, const float* rq,
+                                              uint32_t (&out)[4]) {
+    int x[8];
+    bool slow = false;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const float t = v[r] * rq[8 * r];
+        const float a = fabsf(t);
+        slow |= !(a < 4194304.0f && fabsf(__builtin_amdgcn_fractf(a) - 0.5f) > a * 0x1p-20f);
+        const float n = copysignf(fminf(truncf(a + 0.5f), 32768.0f), t);  // saturating `as i16` below
+        x[r] = (int)fminf(n, 32767.0f);
+    }
+    if (slow) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float a = fabsf(v[r] * rq[8 * r]);
+            if (!(a < 4194304.0f && fabsf(__builtin_amdgcn_fractf(a) - 0.5f) > a * 0x1p-20f))
+                x[r] = quantize(v[r], q[8 * r]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
+}
+
 // arai.rs:7-26 constants, f32 literals as written in the reference
 #define DMMT_A1 0.70710678118654752440f
 #define DMMT_A2 0.5411961f
@@ -374,10 +404,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 for (int i = 0; i < 8; ++i) v[i] = sT[blk * BS + i * 8 + col];
                 arai8(v);
                 const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    qv[jj][i] = (uint32_t)(uint16_t)quantize_rcp(v[2 * i], q[16 * i], rq[16 * i]) |
-                                ((uint32_t)(uint16_t)quantize_rcp(v[2 * i + 1], q[16 * i + 8], rq[16 * i + 8]) << 16);
+                quantize_col8(v, q, rq, qv[jj]);
             }
         }
         __syncthreads();  // every column read: the int16 image may now overwrite sT
