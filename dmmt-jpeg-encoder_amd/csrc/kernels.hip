@@ -143,7 +143,10 @@ __device__ __forceinline__ void rgb_to_ycbcr(float r, float g, float b, float& y
 // aligned 16-byte chunks that cover it at any alignment (byte loads only for a
 // chunk that crosses the frame's first or last byte).  Chunk q of a tile is
 // chunk q % RC of tile row q / RC; thread t owns chunks t, t+256, ...  In LDS a
-// tile row starts at row * RS, its first pixel `misalign` bytes further.
+// tile row starts at row * RS, its first pixel `misalign` bytes further.  Every
+// byte of a tile row past the image's right edge, and every row past its bottom,
+// stages as 0: sample 0 normalises to 0.0, the reference's black padding
+// (padder.rs:12-42), so phase A needs no bounds checks.
 template <typename Sample, int ROWS>
 struct RawTile {
     static constexpr int RB = 256 * 3 * (int)sizeof(Sample);
@@ -179,6 +182,16 @@ struct RawTile {
                 uint32_t w[4] = {0u, 0u, 0u, 0u};
                 for (int k = 0; k < 16; ++k)
                     if (c + k >= 0 && c + k < fbytes) w[k >> 2] |= (uint32_t)fbase[c + k] << (8 * (k & 3));
+                v[i] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            const long long keep = start + rowbytes - c;  // bytes of the chunk inside the tile row
+            if (keep < 16) {  // zero the rest: past the image's right edge the tile reads black
+                uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const long long n = keep - 4 * k;
+                    w[k] &= n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << (8 * n)) - 1u);
+                }
                 v[i] = make_uint4(w[0], w[1], w[2], w[3]);
             }
         }
@@ -312,6 +325,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
             }
             float yv[VR][HR][8];
             float cbv[8], crv[8];
+            uint32_t smax = 0;  // largest sample of the job (a sample above maxval panics in color.rs:63-65)
 #pragma unroll
             for (int k = 0; k < 8; ++k) {  // chroma sample k of the row
                 float cbs = 0.0f, crs = 0.0f;
@@ -320,16 +334,12 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
 #pragma unroll
                     for (int dy = 0; dy < VR; ++dy) {
                         const int jx = k * HR + dx;  // pixel within the job row
-                        const int px = x0 + lx0 + jx;
-                        const int py = y0 + r * VR + dy;
-                        float rr = 0.0f, gg = 0.0f, bb = 0.0f;
-                        if constexpr (SB == 4) {  // Image<f32> dots as given
-                            if (px < g.width && py < g.height) {
-                                rr = fsrc[dy][jx * 3];
-                                gg = fsrc[dy][jx * 3 + 1];
-                                bb = fsrc[dy][jx * 3 + 2];
-                            }
-                        } else if (px < g.width && py < g.height) {
+                        float rr, gg, bb;
+                        if constexpr (SB == 4) {  // Image<f32> dots as given (0.0 past the edges)
+                            rr = fsrc[dy][jx * 3];
+                            gg = fsrc[dy][jx * 3 + 1];
+                            bb = fsrc[dy][jx * 3 + 2];
+                        } else {
                             uint32_t sv[3];
 #pragma unroll
                             for (int ch = 0; ch < 3; ++ch) {
@@ -337,8 +347,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                                 sv[ch] = SB == 1 ? (pw[dy][si >> 2] >> (8 * (si & 3))) & 0xFFu
                                                  : (pw[dy][si >> 1] >> (16 * (si & 1))) & 0xFFFFu;
                             }
-                            bad |= (int)(sv[0] > (uint32_t)g.maxval) | (int)(sv[1] > (uint32_t)g.maxval) |
-                                   (int)(sv[2] > (uint32_t)g.maxval);
+                            smax = max(smax, max(sv[0], max(sv[1], sv[2])));
                             if (SB == 1) {
                                 rr = sLut[sv[0]];
                                 gg = sLut[sv[1]];
@@ -368,6 +377,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 cbv[k] = cbs;
                 crv[k] = crs;
             }
+            bad |= (int)(smax > (uint32_t)g.maxval);
 #pragma unroll
             for (int dy = 0; dy < VR; ++dy) {
                 const int ly = r * VR + dy;
@@ -973,7 +983,7 @@ __global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coe
 namespace dmmt {
 
 #ifndef FRONT_WPE_420
-#define FRONT_WPE_420 1
+#define FRONT_WPE_420 3
 #endif
 
 static inline int clampi(long long v, int lo, int hi) { return (int)(v < lo ? lo : (v > hi ? hi : v)); }
