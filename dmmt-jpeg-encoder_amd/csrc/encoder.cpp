@@ -116,7 +116,11 @@ int ensure(DevBuf& b, size_t bytes, bool zero = false) {
     b.bytes = 0;
     HIP_TRY(hipMalloc(&b.p, bytes));
     b.bytes = bytes;
-    if (zero) HIP_TRY(hipMemset(b.p, 0, bytes));
+    if (zero) {
+        // on the null stream: finished before any lane (non-blocking streams) runs on it
+        HIP_TRY(hipMemset(b.p, 0, bytes));
+        HIP_TRY(hipDeviceSynchronize());
+    }
     return DMMT_OK;
 }
 

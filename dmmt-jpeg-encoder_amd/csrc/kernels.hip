@@ -99,6 +99,35 @@ __device__ __forceinline__ void quantize_col8(const float (&v)[8], const float* 
     for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
 }
 
+// quantize_col8 for integer samples, whose coefficients are bounded: the samples
+// normalise into [0, 1] (a larger one is an error, color.rs:63-65), so Y, Cb, Cr
+// lie in [-128, 128] and every FDCT output in [-2048, 2048] (DC = sum / 8, AC
+// at most (1/4) * 64 * 128), to within a few ulps.  With q >= 1, a = |d/q| <= 2049:
+// |d * (1/q) - fl(d/q)| <= 3 * 2^-24 * a < 2^-11, so outside 2^-10 of a half-integer
+// both round to the same integer, and as t is then no tie, rint (half to even)
+// is round half away from zero; the saturation of `as i16` cannot trigger.
+// Lanes near a half-integer (or NaN: maxval 0) take the division afterwards.
+__device__ __forceinline__ void quantize_col8_bounded(const float (&v)[8], const float* q, const float* rq,
+                                                      uint32_t (&out)[4]) {
+    int x[8];
+    bool slow = false;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const float t = v[r] * rq[8 * r];
+        slow |= !(fabsf(__builtin_amdgcn_fractf(fabsf(t)) - 0.5f) > 0x1p-10f);
+        x[r] = (int)__builtin_rintf(t);
+    }
+    if (slow) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float t = v[r] * rq[8 * r];
+            if (!(fabsf(__builtin_amdgcn_fractf(fabsf(t)) - 0.5f) > 0x1p-10f)) x[r] = quantize(v[r], q[8 * r]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
+}
+
 // arai.rs:7-26 constants, f32 literals as written in the reference
 #define DMMT_A1 0.70710678118654752440f
 #define DMMT_A2 0.5411961f
@@ -414,7 +443,10 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 for (int i = 0; i < 8; ++i) v[i] = sT[blk * BS + i * 8 + col];
                 arai8(v);
                 const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
-                quantize_col8(v, q, rq, qv[jj]);
+                if constexpr (SB == 4)  // Image<f32> dots: unbounded coefficients
+                    quantize_col8(v, q, rq, qv[jj]);
+                else
+                    quantize_col8_bounded(v, q, rq, qv[jj]);
             }
         }
         __syncthreads();  // every column read: the int16 image may now overwrite sT
