@@ -143,6 +143,52 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
         dist.destroy_process_group()
 
 
+def p3_bytes(rgb, maxval=255, sep=b" "):
+    """a P3 file of an (h, w, 3) uint8 image, built vectorised: every sample in decimal
+    followed by one separator byte (the ingest workload of --ppm and its tests)"""
+    h, w, _ = rgb.shape
+    v = np.asarray(rgb, np.int64).reshape(-1)
+    nd = 1 + (v >= 10) + (v >= 100)
+    end = np.cumsum(nd + 1)  # one past each token's separator
+    body = np.full(int(end[-1]) if v.size else 0, sep[0], np.uint8)
+    last = end - 2           # each token's last digit
+    body[last] = 48 + v % 10
+    m = nd >= 2
+    body[last[m] - 1] = 48 + (v[m] // 10) % 10
+    m = nd >= 3
+    body[last[m] - 2] = 48 + v[m] // 100
+    return b"P3\n%d %d\n%d\n" % (w, h, maxval) + body.tobytes()
+
+
+def ppm_ingest(enc, w, h, steps):
+    """SURVEY.md 8(f) row 1, timed apart from the encode (8(d)): one w x h frame of
+    the synthetic workload as a P3 file (one space after every sample) in HBM ->
+    its u8 samples in HBM, dmmt_decode_ppm_device per step (which synchronises).
+    Algorithmic bytes: the file read once + the samples written once."""
+    d_rgb = enc.malloc(w * h * 3)
+    enc.fill_synthetic(d_rgb, w, h, 1)
+    enc.synchronize()
+    rgb = np.frombuffer(enc.d2h(d_rgb, w * h * 3), np.uint8).reshape(h, w, 3)
+    text = p3_bytes(rgb)
+    hdr = dmmt_jpeg.parse_ppm_header(text)
+    d_text = enc.malloc(len(text))
+    enc.h2d(d_text, np.frombuffer(text, np.uint8))
+    for _ in range(3):
+        enc.decode_ppm_device(d_text, len(text), hdr, d_rgb)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        enc.decode_ppm_device(d_text, len(text), hdr, d_rgb)
+    dt = (time.perf_counter() - t0) / steps
+    ok = bytes(enc.d2h(d_rgb, w * h * 3)) == rgb.tobytes()
+    enc.free(d_text)
+    enc.free(d_rgb)
+    algo = len(text) + w * h * 3
+    return {"workload": f"{w}x{h} P3 text ({len(text)} B) in HBM -> u8 samples in HBM, per call incl. its sync",
+            "ms": round(dt * 1e3, 4), "mpixel_per_s": round(w * h / dt / 1e6, 1),
+            "achieved_gbs": round(algo / dt / 1e9, 1), "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes": algo, "samples_match": ok}
+
+
 def stage_index(name):
     L = dmmt_jpeg.lib()
     for i in range(L.dmmt_num_stages()):
@@ -181,6 +227,8 @@ def main(argv=None, make_encoder=None, emit=None):
     ap.add_argument("--config", default="4k444q90", choices=sorted(CONFIGS) + sorted(STRIPED))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--distinct-frames", type=int, default=4)
+    ap.add_argument("--ppm-steps", type=int, default=20,
+                    help="PPM ingest line: P3 decodes of one synthetic frame timed on rank 0 (0 = skip)")
     ap.add_argument("--lanes", type=int, default=4,
                     help="pipeline lanes: consecutive steps overlap on this many workspaces/streams (1 = serial)")
     args = ap.parse_args(argv)
@@ -285,6 +333,7 @@ def main(argv=None, make_encoder=None, emit=None):
                 traffic = json.load(open(pmc)).get("front_hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        ingest = ppm_ingest(enc, w, h, args.ppm_steps) if args.ppm_steps > 0 else None
         cpu = None
         if args.cpu_seconds > 0:
             from oracle.synth import synthetic  # numpy twin of the device generator
@@ -326,6 +375,7 @@ def main(argv=None, make_encoder=None, emit=None):
                          "frac": round(path_achieved / HBM_PEAK_GBS, 4)},
             },
             "cpu_baseline": cpu,
+            "ppm_ingest": ingest,
         }
         emit(json.dumps(line))
     for p in d_in + d_out + d_len:

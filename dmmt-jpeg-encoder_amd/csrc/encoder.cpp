@@ -6,7 +6,9 @@
 // included) is produced on the GPU; there is no CPU fallback -- without a
 // gfx950 device dmmt_ctx_create fails with DMMT_E_NO_DEVICE.
 #include <hip/hip_runtime.h>
+#include <errno.h>
 #include <stdio.h>
+#include <sys/stat.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -66,6 +68,8 @@ struct dmmt_ctx {
     DevBuf status, lut, qtab, qtab_u8;
     // host-API staging
     DevBuf in, out, out_len, dct;
+    // PPM ingest: file bytes, chunk maps / entry states, status + token count
+    DevBuf ppm_text, ppm_maps, ppm_chunk_in, ppm_counts, ppm_misc;
     // uploaded table state
     int lut_maxval = -1, lut_sb = -1;
     uint8_t q_cached[128];
@@ -686,27 +690,106 @@ extern "C" int dmmt_dct_transform(dmmt_ctx* c, float* blocks, size_t len) {
     return DMMT_OK;
 }
 
+// The body of a PPM file already in device memory -> its raw samples (d_rgb), with
+// the reference's error precedence: a token that does not parse (ppm.rs:247-251),
+// an incomplete last pixel (ppm.rs:239-245), a pixel count other than the header's
+// (ppm.rs:165-175), then a P3 sample above maxval (color.rs:63-65).
+static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt_ppm_header* h, void* d_rgb,
+                      hipStream_t st) {
+    int rc;
+    const unsigned long long ns = (unsigned long long)h->width * h->height * 3ull;
+    const int sb = h->maxval > 255 ? 2 : 1;
+    if (h->body_offset > len) return DMMT_E_INVALID_ARGUMENT;
+    if ((rc = ensure(c->ppm_misc, 64, true))) return rc;
+    uint64_t misc[4] = {0, 0, 0, 0};  // PpmMisc: status | status_fast << 32, tokens, flag
+    if (h->binary) {  // P6 (extension): raw big-endian samples after the header, as dmmt_parse_ppm
+        if (len - h->body_offset < ns * (unsigned long long)sb) return DMMT_E_PPM_SIZE_MISMATCH;
+        HIP_TRY(launch_ppm_p6(d_text + h->body_offset, d_rgb, sb, ns, h->maxval, nullptr, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return DMMT_OK;
+    }
+    const size_t nch = ppm_chunk_count(d_text, h->body_offset, len);
+    if ((rc = ensure(c->ppm_maps, std::max<size_t>(nch, 1024) * 8))) return rc;
+    if ((rc = ensure(c->ppm_chunk_in, std::max<size_t>(nch, 1024) * 8))) return rc;
+    if ((rc = ensure(c->ppm_counts, ppm_counts_capacity((long long)nch) * 4))) return rc;
+    HIP_TRY(launch_ppm_p3(d_text, h->body_offset, len, (unsigned long long*)c->ppm_maps.p,
+                          (unsigned long long*)c->ppm_chunk_in.p, (uint32_t*)c->ppm_counts.p, c->ppm_misc.p,
+                          d_rgb, sb, ns, h->maxval, st));
+    HIP_TRY(hipMemcpyAsync(misc, c->ppm_misc.p, 24, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const bool comments = (uint32_t)misc[2] != 0;
+    const uint32_t s = comments ? (uint32_t)misc[0] : (uint32_t)(misc[0] >> 32);
+    if (s & 1u) return DMMT_E_PPM_PARSE_TOKEN;
+    if (misc[1] % 3) return DMMT_E_PPM_INCOMPLETE_PIXEL;
+    if (misc[1] != ns) return DMMT_E_PPM_SIZE_MISMATCH;
+    if (s & 2u) return DMMT_E_VALUE_EXCEEDS_MAX;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_decode_ppm_device(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt_ppm_header* h,
+                                      void* d_rgb, void* stream) {
+    if (!c || !h || (!d_text && len) || (!d_rgb && h->width && h->height)) return DMMT_E_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    return decode_ppm(c, d_text, len, h, d_rgb, stream ? (hipStream_t)stream : c->stream);
+}
+
 extern "C" int dmmt_convert_ppm_to_jpeg(dmmt_ctx* c, const char* input_path, const char* output_path,
                                         const dmmt_options* opt) {
-    // lib.rs:59-77: open input, open output, read PPM, encode, write
+    // lib.rs:59-77: open input, open output, read PPM, encode, write.  The file's
+    // bytes go to the GPU as they are: the samples are decoded there
+    // (dmmt_decode_ppm_device) and encoded from device memory.
     if (!c || !input_path || !output_path) return DMMT_E_INVALID_ARGUMENT;
-    FILE* probe = fopen(input_path, "rb");
-    if (!probe) return DMMT_E_OPEN_INPUT;
-    fclose(probe);
-    FILE* fo = fopen(output_path, "wb");
-    if (!fo) return DMMT_E_OPEN_OUTPUT;
-    dmmt_image img;
-    int rc = dmmt_read_ppm(input_path, &img);
-    if (rc) {
-        fclose(fo);
-        return rc;
+    int rc;
+    if ((rc = validate(opt))) return rc;
+    FILE* fi = fopen(input_path, "rb");  // open_input_file (lib.rs:43-47)
+    if (!fi) return DMMT_E_OPEN_INPUT;
+    FILE* fo = fopen(output_path, "wb");  // open_output_file (lib.rs:49-57)
+    if (!fo) {
+        fclose(fi);
+        return DMMT_E_OPEN_OUTPUT;
     }
-    uint8_t* jpg = nullptr;
-    size_t n = 0;
-    rc = dmmt_jpeg_encode(c, &img, opt, &jpg, &n);
-    free((void*)img.rgb);
-    if (rc == DMMT_OK && fwrite(jpg, 1, n, fo) != n) rc = DMMT_E_WRITE_IMAGE_DATA;
-    free(jpg);
+    std::vector<uint8_t> data;
+    struct stat sst;
+    rc = fstat(fileno(fi), &sst) == 0 ? DMMT_OK : DMMT_E_OPEN_INPUT;
+    if (!rc) {
+        data.resize((size_t)sst.st_size);
+        if ((data.empty() ? 0 : fread(data.data(), 1, data.size(), fi)) != data.size()) rc = DMMT_E_OPEN_INPUT;
+    }
+    fclose(fi);
+    dmmt_ppm_header h;
+    if (!rc) rc = dmmt_parse_ppm_header(data.data(), data.size(), &h);
+    std::vector<uint8_t> jpg;
+    if (!rc) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipStream_t st = c->stream;
+        const int sb = h.maxval > 255 ? 2 : 1;
+        const size_t frame_bytes = (size_t)h.width * h.height * 3 * (size_t)sb;
+        if (!(rc = set_device(c)) && !(rc = ensure(c->ppm_text, data.size())) &&
+            !(rc = ensure(c->in, frame_bytes)) &&
+            !(rc = hip_err(hipMemcpyAsync(c->ppm_text.p, data.data(), data.size(), hipMemcpyHostToDevice, st))))
+            rc = decode_ppm(c, (const uint8_t*)c->ppm_text.p, data.size(), &h, c->in.p, st);
+        if (!rc && (h.width == 0 || h.height == 0)) rc = DMMT_E_INVALID_ARGUMENT;  // as check_image
+        Geom g;
+        if (!rc) rc = make_checked_geom(h.width, h.height, opt->subsampling, h.maxval, opt->restart_interval, &g);
+        if (!rc) {
+            const size_t out_stride = (max_jpeg_bytes(g) + 255) / 256 * 256;
+            if (!(rc = ensure(c->out, out_stride)) && !(rc = ensure(c->out_len, sizeof(uint32_t))))
+                rc = enqueue_encode(c, c->in.p, frame_bytes, sb, 1, g, opt, (uint8_t*)c->out.p, out_stride,
+                                    (uint32_t*)c->out_len.p, st);
+            uint32_t L = 0;
+            if (!rc) rc = hip_err(hipMemcpyAsync(&L, c->out_len.p, 4, hipMemcpyDeviceToHost, st));
+            if (!rc) rc = hip_err(hipStreamSynchronize(st));
+            if (!rc) rc = take_status(c, st);
+            if (!rc && (L == 0 || L > out_stride)) rc = DMMT_E_CAPACITY;
+            if (!rc) {
+                jpg.resize(L);
+                rc = hip_err(hipMemcpy(jpg.data(), c->out.p, L, hipMemcpyDeviceToHost));
+            }
+        }
+    }
+    if (rc == DMMT_OK && fwrite(jpg.data(), 1, jpg.size(), fo) != jpg.size()) rc = DMMT_E_WRITE_IMAGE_DATA;
     if (fclose(fo) != 0 && rc == DMMT_OK) rc = DMMT_E_WRITE_END_OF_FILE;
     return rc;
 }

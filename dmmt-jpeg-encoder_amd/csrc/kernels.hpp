@@ -42,6 +42,20 @@ hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t s
 hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_t st);
 hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
                              uint32_t* out_len, hipStream_t st);
+// P3 body decoding (ppm_device.hip): text [body_offset, len) -> nsamples samples of
+// sample_bytes each.  misc (32 bytes, PpmMisc): u32 status of the general path, u32
+// status of the comment-free path (bits: 1 parse error, 2 sample above maxval),
+// u64 tokens found, u32 comment flag.  With n = ppm_chunk_count(...): maps and
+// chunk_in 8 max(n, 1024) bytes each, counts 4 ppm_counts_capacity(n) bytes.
+size_t ppm_chunk_count(const uint8_t* text, size_t body_offset, size_t len);
+size_t ppm_counts_capacity(long long nch);
+hipError_t launch_ppm_p3(const uint8_t* text, size_t body_offset, size_t len, unsigned long long* maps,
+                         unsigned long long* chunk_in, uint32_t* counts, void* misc, void* out, int sample_bytes,
+                         unsigned long long nsamples, uint32_t maxval, hipStream_t st);
+// P6 samples (big-endian u16 or u8) already in device memory -> host-endian samples
+// (maxval and status unused: the encoder checks the range, as for dmmt_parse_ppm)
+hipError_t launch_ppm_p6(const uint8_t* samples, void* out, int sample_bytes, unsigned long long nsamples,
+                         uint32_t maxval, uint32_t* status, hipStream_t st);
 hipError_t launch_dct_blocks(float* data, long long nblocks, hipStream_t st);
 hipError_t launch_synthetic(uint8_t* rgb, int w, int h, int n_frames, int first_frame, uint32_t seed, int row0,
                             int rows, hipStream_t st);

@@ -62,11 +62,11 @@ bool parse_u16(const std::string& t, uint16_t* out) {
 
 }  // namespace
 
-extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) {
-    if (!img || (!data && len)) return DMMT_E_INVALID_ARGUMENT;
-    memset(img, 0, sizeof *img);
-    Tokenizer tz{data, len};
+// parse_header .. parse_max_value (ppm.rs:145-222): the four header tokens; the
+// body starts after the whitespace byte that ended the max value
+static int parse_header(Tokenizer& tz, dmmt_ppm_header* hdr) {
     std::string tok;
+    memset(hdr, 0, sizeof *hdr);
     // parse_header + check_header_version (ppm.rs:177-192)
     if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
     const bool binary = tok == "P6";
@@ -78,6 +78,30 @@ extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) 
     if (!parse_u16(tok, &h)) return DMMT_E_PPM_PARSE_TOKEN;
     if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
     if (!parse_u16(tok, &mx)) return DMMT_E_PPM_PARSE_TOKEN;
+    hdr->width = w;
+    hdr->height = h;
+    hdr->maxval = mx;
+    hdr->binary = binary ? 1 : 0;
+    hdr->body_offset = tz.i;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_parse_ppm_header(const uint8_t* data, size_t len, dmmt_ppm_header* hdr) {
+    if (!hdr || (!data && len)) return DMMT_E_INVALID_ARGUMENT;
+    Tokenizer tz{data, len};
+    return parse_header(tz, hdr);
+}
+
+extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) {
+    if (!img || (!data && len)) return DMMT_E_INVALID_ARGUMENT;
+    memset(img, 0, sizeof *img);
+    Tokenizer tz{data, len};
+    std::string tok;
+    dmmt_ppm_header hdr;
+    int rc = parse_header(tz, &hdr);
+    if (rc) return rc;
+    const bool binary = hdr.binary != 0;
+    const uint16_t w = hdr.width, h = hdr.height, mx = hdr.maxval;
     const size_t npx = (size_t)w * h;
     const int sb = mx > 255 ? 2 : 1;
     uint8_t* buf = (uint8_t*)malloc(npx * 3 * (size_t)sb + 1);

@@ -1,0 +1,693 @@
+// ppm_device.hip -- gfx950 decoding of a P3 body (the ASCII samples after the header)
+// straight into the raw sample image in HBM.  [ppm.rs:41-77 PPMTokenizer::next,
+// ppm.rs:224-252 parse_all_dots / parse_color_value, ppm.rs:165-175 size check]
+//
+// The reference tokenizer, exactly: a '#' outside a comment starts one that runs
+// up to and including the next '\n' and is dropped WITHOUT ending the current
+// token ("12#x\n34" is the token "1234"); ASCII whitespace (space, \t, \n, \x0C,
+// \r) ends a token; every token must parse as a u16 (Rust `str::parse::<u16>`:
+// an optional '+', then decimal digits, value <= 65535).
+//
+// The text is cut into chunks of 4096 bytes (256 threads x 16 bytes).  What a
+// chunk does depends only on the state the text is in where it starts: inside a
+// comment or not, and whether the last kept (non-comment) byte before it was a
+// token byte.  Three launches:
+//  k_ppm_summary  every chunk's transition map: for each of the 4 entry states,
+//                 the exit state and the number of tokens starting in the chunk
+//                 (per thread from 16-bit byte-class masks, composed in order
+//                 over the workgroup)
+//  k_ppm_carry    one workgroup: ordered scan of the maps -> each chunk's entry
+//                 state and the index of its first token; the token count
+//  k_ppm_parse    every chunk again: token starts at its real entry state, each
+//                 token parsed by the thread it starts in (reading on past the
+//                 chunk when it must) and written at its index as u8 / u16;
+//                 parse errors and samples above maxval as status bits
+// A 16-byte window with no '#' (the normal case) is classified by mask
+// arithmetic; one with a '#' is walked byte by byte.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+namespace dmmt {
+
+constexpr int kPpmWin = 16;                    // bytes per thread
+constexpr int kPpmThreads = 256;
+constexpr int kPpmChunk = kPpmWin * kPpmThreads;  // bytes per workgroup
+constexpr int kPpmTail = 256;                  // bytes staged past the chunk for tokens running on
+constexpr int kPpmCarryThreads = 1024;
+
+// Transition maps: entry state s = (in comment) << 1 | (last kept byte a token
+// byte); entry s occupies bits [16s, 16s + 16): exit state << 14 | tokens started.
+constexpr unsigned long long kMapIdentity = 0xC000800040000000ull;
+
+__device__ __forceinline__ unsigned long long map_compose(unsigned long long f, unsigned long long g) {
+    unsigned long long h = 0;  // f, then g
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const uint32_t e = (uint32_t)(f >> (16 * s)) & 0xFFFFu;
+        const uint32_t e2 = (uint32_t)(g >> (16 * (e >> 14))) & 0xFFFFu;
+        h |= (unsigned long long)((e2 & 0xC000u) | ((e & 0x3FFFu) + (e2 & 0x3FFFu))) << (16 * s);
+    }
+    return h;
+}
+
+__device__ __forceinline__ bool ppm_ws(uint32_t b) {  // char::is_ascii_whitespace
+    return b == 32u || (b - 9u < 5u && b != 11u);
+}
+
+// One thread's 16 bytes, as bit masks (bit i = byte i)
+struct PpmWin {
+    uint32_t w[4];
+    uint32_t valid, ws, hash, nl;
+    __device__ __forceinline__ uint32_t byte(int i) const { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
+};
+
+// Window at text offset `pos` (16-aligned relative to `text`), bytes [lo, len)
+// valid; bytes before `safe` are outside the caller's buffer and never read.
+__device__ __forceinline__ void ppm_window(const uint8_t* __restrict__ text, long long pos, long long lo,
+                                           long long len, long long safe, PpmWin& W) {
+    W.valid = 0;
+    W.w[0] = W.w[1] = W.w[2] = W.w[3] = 0u;
+    if (pos + kPpmWin <= lo || pos >= len) {
+        W.ws = W.hash = W.nl = 0;
+        return;
+    }
+    if (pos >= safe && pos + kPpmWin <= len) {
+        const uint4 v = *reinterpret_cast<const uint4*>(text + pos);
+        W.w[0] = v.x;
+        W.w[1] = v.y;
+        W.w[2] = v.z;
+        W.w[3] = v.w;
+    } else {
+        for (int k = 0; k < kPpmWin; ++k)
+            if (pos + k >= lo && pos + k < len) W.w[k >> 2] |= (uint32_t)text[pos + k] << (8 * (k & 3));
+    }
+    const long long a = lo > pos ? lo - pos : 0, b = len - pos < kPpmWin ? len - pos : kPpmWin;
+    W.valid = ((1u << (int)b) - 1u) & ~((1u << (int)a) - 1u);
+    uint32_t ws = 0, hash = 0, nl = 0;
+#pragma unroll
+    for (int i = 0; i < kPpmWin; ++i) {
+        const uint32_t c = W.byte(i);
+        ws |= (uint32_t)ppm_ws(c) << i;
+        hash |= (uint32_t)(c == 0x23u) << i;
+        nl |= (uint32_t)(c == 0x0Au) << i;
+    }
+    W.ws = ws & W.valid;
+    W.hash = hash & W.valid;
+    W.nl = nl & W.valid;
+}
+
+// The window from entry state s: its token starts (bit mask) and exit state.
+__device__ __forceinline__ uint32_t ppm_step(const PpmWin& W, int s, uint32_t& starts) {
+    const int c = s >> 1, sg = s & 1;
+    uint32_t kept;
+    bool fast;
+    if (c) {
+        if (!W.nl) {  // the whole window is comment
+            starts = 0;
+            return (uint32_t)s;
+        }
+        kept = W.valid & ~((2u << __builtin_ctz(W.nl)) - 1u);  // after the '\n' that ends it
+        fast = (W.hash & kept) == 0;
+    } else {
+        kept = W.valid;
+        fast = W.hash == 0;
+    }
+    if (fast) {
+        const uint32_t sig = kept & ~W.ws;
+        const uint32_t first = kept & (0u - kept);
+        starts = sig & ~((sig << 1) | (sg ? first : 0u));
+        return kept ? (sig >> (31 - __clz((int)kept))) & 1u : (uint32_t)sg;
+    }
+    int cc = c, ss = sg;
+    uint32_t st = 0;
+    for (int i = 0; i < kPpmWin; ++i) {
+        if (!((W.valid >> i) & 1u)) continue;
+        const uint32_t b = W.byte(i);
+        if (cc) {
+            if (b == 0x0Au) cc = 0;
+            continue;
+        }
+        if (b == 0x23u) {
+            cc = 1;
+            continue;
+        }
+        if (ppm_ws(b)) {
+            ss = 0;
+        } else {
+            if (!ss) st |= 1u << i;
+            ss = 1;
+        }
+    }
+    starts = st;
+    return (uint32_t)(cc << 1 | ss);
+}
+
+__device__ __forceinline__ unsigned long long ppm_window_map(const PpmWin& W) {
+    unsigned long long m = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        uint32_t st;
+        const uint32_t x = ppm_step(W, s, st);
+        m |= (unsigned long long)((x << 14) | (uint32_t)__popc(st)) << (16 * s);
+    }
+    return m;
+}
+
+__device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, int d) {
+    return ((unsigned long long)(uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64) << 32) |
+           (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
+}
+
+// Exclusive ordered scan of the 256 window maps of a workgroup; also the whole.
+__device__ __forceinline__ unsigned long long ppm_block_scan(unsigned long long m, unsigned long long* sWave,
+                                                             unsigned long long& total) {
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    unsigned long long inc = m;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long o = shfl_up_u64(inc, d);
+        if (lane >= d) inc = map_compose(o, inc);
+    }
+    if (lane == 63) sWave[wave] = inc;
+    unsigned long long exc = shfl_up_u64(inc, 1);
+    if (lane == 0) exc = kMapIdentity;
+    __syncthreads();
+    unsigned long long pre = kMapIdentity;
+    for (int q = 0; q < wave; ++q) pre = map_compose(pre, sWave[q]);
+    total = kMapIdentity;
+    for (int q = 0; q < kPpmThreads / 64; ++q) total = map_compose(total, sWave[q]);
+    return map_compose(pre, exc);
+}
+
+struct PpmText {
+    const uint8_t* text;  // chunk 0 starts here (16-aligned)
+    long long lo, len;    // body bytes [lo, len) relative to text
+    long long safe;       // first byte of the caller's buffer relative to text (<= lo)
+    long long nch;
+};
+
+// Comment-free bodies (no '#' after the header: every P3 writer's output) take a
+// fast path in which a token starts at every token byte whose previous byte is
+// whitespace (or the body start), so a chunk's token count is a plain sum and its
+// first token's index a plain prefix sum.  The first launch also raises `flag` if
+// any '#' is present; the transition-map kernels then do the general work (and
+// are empty launches otherwise).
+
+// 0x80 in every byte of y that is zero
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t y) {
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+}
+
+// whitespace bytes of a word (char::is_ascii_whitespace), 4 bits: ' ' by a zero
+// test, 9 10 12 13 as the bytes in 8..15 whose low 3 bits select a 1 in an
+// 8-entry byte table (v_perm_b32)
+__device__ __forceinline__ uint32_t ws4(uint32_t x) {
+    const uint32_t sp = zero_bytes(x ^ 0x20202020u);
+    const uint32_t in8 = zero_bytes((x & 0xF8F8F8F8u) ^ 0x08080808u);
+    const uint32_t lk = __builtin_amdgcn_perm(0x00000101u, 0x00010100u, x & 0x07070707u);
+    const uint32_t h = sp | (in8 & (lk << 7));
+    return ((h >> 7) * 0x10204080u) >> 28;
+}
+
+// A window for the comment-free path: its words, valid bytes, whitespace and
+// whether it holds a '#'
+// whether it holds a '#'.  Lane 0 also reads the byte before the window and lane
+// 63 the 4 bytes after it (their neighbours' windows are in other waves), all
+// loads issued together.
+struct FastWin {
+    uint32_t w[4];
+    uint32_t valid, ws;
+    bool hash;
+    uint32_t prev_sig;   // lane 0: the byte before the window is a token byte
+    uint32_t next_w;     // lane 63: the 4 bytes after the window (0 past the text)
+    uint32_t next_end;   // lane 63: which of them end a token (whitespace, past the text)
+};
+
+__device__ __forceinline__ void fast_window(const PpmText& t, long long pos, FastWin& F, bool want_next) {
+    // Unconditional loads at clamped addresses (inside the caller's buffer: the
+    // launcher guarantees t.len - t.safe >= 32), so all of them are in flight
+    // together; the few windows at the ends of the body are fixed up byte-wise.
+    const int lane = lane_id();
+    const long long s16 = (t.safe + 15) & ~15ll;
+    const bool full = pos >= t.safe && pos + kPpmWin <= t.len;
+    const uint4 v = *reinterpret_cast<const uint4*>(t.text + (full ? pos : s16));
+    const long long qp = min(max(pos - 1, t.lo), t.len - 1);
+    const uint32_t pb = t.text[qp];
+    const long long qn = pos + kPpmWin, qn4 = min(qn, (t.len - 4) & ~3ll);
+    const uint32_t nw = want_next ? *reinterpret_cast<const uint32_t*>(t.text + qn4) : 0u;
+    F.w[0] = full ? v.x : 0u;
+    F.w[1] = full ? v.y : 0u;
+    F.w[2] = full ? v.z : 0u;
+    F.w[3] = full ? v.w : 0u;
+    F.prev_sig = (lane == 0 && pos - 1 >= t.lo && pos - 1 < t.len) ? (uint32_t)!ppm_ws(pb) : 0u;
+    F.next_w = 0u;
+    F.next_end = 0xFu;
+    if (want_next && lane == 63) {
+        if (qn + 4 <= t.len) {
+            F.next_w = nw;
+            F.next_end = ws4(nw);
+        } else {
+            for (int j = 0; j < 4; ++j)
+                if (qn + j < t.len) F.next_w |= (uint32_t)t.text[qn + j] << (8 * j);
+            const long long in = qn < t.len ? t.len - qn : 0;  // bytes of the 4 inside the text
+            F.next_end = (ws4(F.next_w) | ~((1u << (int)in) - 1u)) & 0xFu;
+        }
+    }
+    F.valid = F.ws = 0u;
+    F.hash = false;
+    if (pos + kPpmWin <= t.lo || pos >= t.len) return;
+    if (!full) {
+        for (int k = 0; k < kPpmWin; ++k)
+            if (pos + k >= t.lo && pos + k < t.len) F.w[k >> 2] |= (uint32_t)t.text[pos + k] << (8 * (k & 3));
+    }
+    const long long a = t.lo > pos ? t.lo - pos : 0, b = t.len - pos < kPpmWin ? t.len - pos : kPpmWin;
+    F.valid = ((1u << (int)b) - 1u) & ~((1u << (int)a) - 1u);
+    uint32_t ws = 0, hz = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        ws |= ws4(F.w[k]) << (4 * k);
+        hz |= zero_bytes(F.w[k] ^ 0x23232323u);
+    }
+    F.ws = ws & F.valid;
+    F.hash = hz != 0u;  // (bytes outside the text are 0, never '#')
+}
+
+// this window's token starts when there are no comments: the previous byte is
+// the previous thread's last (a shuffle) or, for lane 0, read back
+__device__ __forceinline__ uint32_t fast_starts(const FastWin& W) {
+    const uint32_t sig = W.valid & ~W.ws;
+    uint32_t prev = (uint32_t)__shfl_up((int)((sig >> 15) & 1u), 1, 64);
+    if (lane_id() == 0) prev = W.prev_sig;
+    return sig & ~((sig << 1) | prev);
+}
+
+
+// ---------------------------------------------------------------- comment-free path
+// Bodies without '#' (every P3 writer's output) in two passes over the text:
+//  k_ppm_count   each chunk's token count (a token starts at every token byte
+//                after whitespace); raises `flag` on any '#'
+//  k_ppm_carry   one workgroup: exclusive sum of the counts (or, with comments,
+//                the transition-map scan of the general path)
+//  k_ppm_fast    each chunk: its tokens parsed from registers -- a token of at
+//                most 4 bytes read with one byte-align from the window's words
+//                (and the next window's first word), digits checked and combined
+//                per byte lane (SWAR); longer ones, '+' and bad tokens take the
+//                byte walk -- staged in LDS in token order and stored coalesced
+// With a '#' anywhere these write nothing that is used: the general kernels
+// (k_ppm_maps, k_ppm_parse) redo the body.
+__device__ __forceinline__ uint32_t pick5(const uint32_t (&w)[5], int j) {
+    return j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : j == 3 ? w[3] : w[4];
+}
+
+// A token from byte p (a token start) to the next kept whitespace, as
+// `str::parse::<u16>` (ppm.rs:247-251): the general byte walk, comments included.
+__device__ __forceinline__ uint32_t parse_token_walk(const PpmText& t, const uint8_t* sText, long long c0,
+                                                     long long p, bool& ok) {  // sText: the staged chunk or null
+    bool comment = false, first = true;
+    int digits = 0;
+    uint32_t v = 0;
+    ok = true;
+    for (; p < t.len; ++p) {
+        const long long r = p - c0;
+        const uint32_t b = sText && r < kPpmChunk + kPpmTail ? sText[r] : t.text[p];
+        if (comment) {
+            if (b == 0x0Au) comment = false;
+            continue;
+        }
+        if (b == 0x23u) {
+            comment = true;
+            continue;
+        }
+        if (ppm_ws(b)) break;
+        if (b - 0x30u < 10u) {
+            v = v * 10u + (b - 0x30u);
+            ok = ok && v <= 65535u;
+            v = min(v, 65536u);
+            ++digits;
+        } else if (!(first && b == 0x2Bu)) {
+            ok = false;
+        }
+        first = false;
+    }
+    ok = ok && digits > 0;
+    return v;
+}
+
+template <typename Out>
+__device__ __forceinline__ void put_sample(Out* out, unsigned long long idx, unsigned long long nsamples, uint32_t v,
+                                           bool ok, uint32_t maxval, uint32_t& bad, uint32_t& over) {
+    bad |= !ok;
+    over |= ok && v > maxval;
+    if (idx < nsamples) out[idx] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+}
+
+
+
+// misc words (zeroed per call): status of the general path, status of the fast
+// path, token count, comment flag, chunk ticket
+struct PpmMisc {
+    uint32_t status, status_fast;
+    unsigned long long tokens;
+    uint32_t flag, ticket;
+};
+
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* __restrict__ counts,
+                                                           PpmMisc* __restrict__ misc) {
+    __shared__ uint32_t sRed[kPpmThreads / 64];
+    const int tid = threadIdx.x;
+    const long long pos = (long long)blockIdx.x * kPpmChunk + (long long)tid * kPpmWin;
+    FastWin F;
+    fast_window(t, pos, F, false);
+    const uint32_t n = wave_sum_u32((uint32_t)__popc(fast_starts(F)));
+    if (lane_id() == 0) sRed[tid >> 6] = n;
+    const bool hash = __syncthreads_or(F.hash) != 0;
+    if (tid == 0) {
+        uint32_t c = 0;
+        for (int q = 0; q < kPpmThreads / 64; ++q) c += sRed[q];
+        counts[blockIdx.x] = c;
+        if (hash) atomicOr(&misc->flag, 1u);
+    }
+}
+
+template <typename Out>
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __restrict__ misc,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const unsigned long long* __restrict__ row_base,
+                                                          long long per, Out* __restrict__ out,
+                                                          unsigned long long nsamples, uint32_t maxval) {
+    __shared__ uint32_t sWave[kPpmThreads / 64];
+    __shared__ unsigned long long sBase;
+    __shared__ Out sOut[kPpmChunk / 2];  // at most one token per two bytes
+    if (misc->flag != 0u) return;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const long long pos = (long long)blockIdx.x * kPpmChunk + (long long)tid * kPpmWin;
+    // the first token's index: the counts before this chunk within its carry row
+    // (wave 0, loads issued beside the window's)
+    const long long row0 = (long long)(blockIdx.x / per) * per, bx = (long long)blockIdx.x;
+    FastWin F;
+    fast_window(t, pos, F, true);
+    const uint32_t c0 = counts[min(row0 + lane, bx)];
+    uint32_t cnt = row0 + lane < bx ? c0 : 0u;
+    for (long long r0 = row0 + 64; r0 < bx; r0 += 64) {  // rows of more than 64 chunks (texts > 256 MB)
+        const uint32_t c = counts[min(r0 + lane, bx)];
+        cnt += r0 + lane < bx ? c : 0u;
+    }
+    uint32_t starts = fast_starts(F);
+    const uint32_t n = (uint32_t)__popc(starts);
+    const uint32_t end16 = (F.ws | ~F.valid) & 0xFFFFu;  // bytes that end a token
+    uint32_t w[5] = {F.w[0], F.w[1], F.w[2], F.w[3], (uint32_t)__shfl_down((int)F.w[0], 1, 64)};
+    uint32_t next4 = (uint32_t)__shfl_down((int)end16, 1, 64) & 0xFu;
+    if (lane == 63) {  // the next window belongs to the next wave (or chunk)
+        w[4] = F.next_w;
+        next4 = F.next_end;
+    }
+    const uint32_t ends = end16 | (next4 << 16);
+    if (wave == 0) {
+        cnt = wave_sum_u32(cnt);
+        if (lane == 0) sBase = row_base[blockIdx.x / per] + cnt;
+    }
+    const uint32_t inc = wave_incl_scan_u32(n);
+    if (lane == 63) sWave[wave] = inc;
+    __syncthreads();
+    uint32_t slot = inc - n, total = 0;
+    for (int q = 0; q < kPpmThreads / 64; ++q) {
+        slot += q < wave ? sWave[q] : 0u;
+        total += sWave[q];
+    }
+    uint32_t bad = 0, over = 0;
+    while (starts) {
+        const int i = __builtin_ctz(starts);
+        starts &= starts - 1u;
+        const uint32_t e = ends >> i;
+        const int L = (e & 0x1Fu) ? __builtin_ctz(e) : 5;
+        uint32_t v = 0;
+        bool ok = false;
+        if (L <= 4) {
+            const int j = i >> 2;
+            const uint32_t x = __builtin_amdgcn_alignbyte(pick5(w, j + 1), pick5(w, j), (uint32_t)(i & 3));
+            const uint32_t m = L == 4 ? 0xFFFFFFFFu : (1u << (8 * L)) - 1u;
+            const uint32_t ge30 = ((x | 0x80808080u) - 0x30303030u) & 0x80808080u;
+            const uint32_t ge3a = ((x & 0x7F7F7F7Fu) + 0x46464646u) & 0x80808080u;
+            ok = (((~ge30 | ge3a | x) & 0x80808080u) & m) == 0u;
+            if (ok) {
+                const uint32_t d = (x & 0x0F0F0F0Fu & m) << (8 * (4 - L));  // leading zero digits
+                const uint32_t t1 = (d & 0x00FF00FFu) * 10u + ((d >> 8) & 0x00FF00FFu);
+                v = (t1 & 0xFFFFu) * 100u + (t1 >> 16);
+            }
+        }
+        if (!ok) v = parse_token_walk(t, nullptr, 0, pos + i, ok);  // '+', long, or not a number
+        bad |= !ok;
+        over |= ok && v > maxval;
+        sOut[slot++] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+    }
+    __syncthreads();
+    const unsigned long long base = sBase;
+    const unsigned long long lim = base < nsamples ? min((unsigned long long)total, nsamples - base) : 0ull;
+    for (uint32_t i = tid; i < lim; i += kPpmThreads) out[base + i] = sOut[i];  // consecutive lanes, bytes
+    if (bad) atomicOr(&misc->status_fast, 1u);
+    if (over) atomicOr(&misc->status_fast, 2u);
+}
+
+// ---------------------------------------------------------------- general path
+// Only when the body holds a '#' (misc->flag); otherwise each is an empty launch
+// of kPpmGeneralGrid workgroups.
+constexpr int kPpmGeneralGrid = 256;
+
+// every chunk's transition map
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_maps(PpmText t, const PpmMisc* __restrict__ misc,
+                                                          unsigned long long* __restrict__ maps) {
+    __shared__ unsigned long long sWave[kPpmThreads / 64];
+    if (misc->flag == 0u) return;
+    for (long long k = blockIdx.x; k < t.nch; k += gridDim.x) {
+        const long long pos = k * kPpmChunk + (long long)threadIdx.x * kPpmWin;
+        PpmWin W;
+        ppm_window(t.text, pos, t.lo, t.len, t.safe, W);
+        unsigned long long total;
+        (void)ppm_block_scan(ppm_window_map(W), sWave, total);
+        if (threadIdx.x == 0) maps[k] = total;
+        __syncthreads();  // sWave reused by the next chunk
+    }
+}
+
+// Chunk-range maps with 64-bit counts: exit state in bits 62-63 of each entry.
+struct WideMap {
+    unsigned long long e[4];
+};
+
+__device__ __forceinline__ WideMap wide_identity() {
+    WideMap m;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) m.e[s] = (unsigned long long)s << 62;
+    return m;
+}
+
+__device__ __forceinline__ WideMap wide_compose(const WideMap& f, const WideMap& g) {
+    WideMap h;
+    constexpr unsigned long long kCnt = (1ull << 62) - 1ull;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const unsigned long long e = f.e[s];
+        const int x = (int)(e >> 62);
+        const unsigned long long e2 = x == 0 ? g.e[0] : x == 1 ? g.e[1] : x == 2 ? g.e[2] : g.e[3];
+        h.e[s] = (e2 & ~kCnt) | ((e & kCnt) + (e2 & kCnt));
+    }
+    return h;
+}
+
+__device__ __forceinline__ WideMap widen(unsigned long long m) {
+    WideMap w;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const uint32_t e = (uint32_t)(m >> (16 * s)) & 0xFFFFu;
+        w.e[s] = ((unsigned long long)(e >> 14) << 62) | (e & 0x3FFFu);
+    }
+    return w;
+}
+
+// chunk_in[k] = entry state << 62 | index of the chunk's first token; the token count
+__global__ __launch_bounds__(kPpmCarryThreads) void k_ppm_carry(const uint32_t* __restrict__ counts,
+                                                                const unsigned long long* __restrict__ maps,
+                                                                long long nch, long long rper,
+                                                                PpmMisc* __restrict__ misc,
+                                                                unsigned long long* __restrict__ chunk_in) {
+    __shared__ WideMap sScan[kPpmCarryThreads];
+    const int t = threadIdx.x;
+    const long long per = (nch + kPpmCarryThreads - 1) / kPpmCarryThreads;
+    const long long k0 = min((long long)t * per, nch), k1 = min(k0 + per, nch);
+    if (misc->flag == 0u) {
+        // comment-free: thread t's row = chunks [t*rper, (t+1)*rper) (rper a multiple
+        // of 4: 16-byte loads; the counts buffer is padded), its exclusive sum ->
+        // row_base[t]; k_ppm_fast adds the counts before it within its row
+        unsigned long long* sSum = reinterpret_cast<unsigned long long*>(sScan);
+        const long long r0 = (long long)t * rper;
+        unsigned long long s = 0;
+        for (long long kb = r0; kb < r0 + rper; kb += 16) {
+            uint4 c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = *reinterpret_cast<const uint4*>(counts + kb + 4 * u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long long k = kb + 4 * u;
+                s += (k < nch ? c[u].x : 0u) + (k + 1 < nch ? c[u].y : 0u) + (k + 2 < nch ? c[u].z : 0u) +
+                     (k + 3 < nch ? c[u].w : 0u);
+                if (kb + 4 * u + 4 >= r0 + rper) break;
+            }
+        }
+        const unsigned long long inc = wave_incl_scan_u64(s);
+        if (lane_id() == 63) sSum[t >> 6] = inc;
+        __syncthreads();
+        unsigned long long base = inc - s;
+        for (int q = 0; q < (t >> 6); ++q) base += sSum[q];
+        chunk_in[t] = base;  // the row bases
+        if (t == kPpmCarryThreads - 1) misc->tokens = base + s;
+        return;
+    }
+    WideMap m = wide_identity();
+    for (long long k = k0; k < k1; ++k) m = wide_compose(m, widen(maps[k]));
+    sScan[t] = m;
+    __syncthreads();
+    for (int d = 1; d < kPpmCarryThreads; d <<= 1) {  // Hillis-Steele, inclusive
+        WideMap o = wide_identity();
+        if (t >= d) o = sScan[t - d];
+        __syncthreads();
+        if (t >= d) sScan[t] = wide_compose(o, sScan[t]);
+        __syncthreads();
+    }
+    const WideMap pre = t ? sScan[t - 1] : wide_identity();
+    unsigned long long cur = pre.e[0];  // the body starts outside a comment, after whitespace
+    for (long long k = k0; k < k1; ++k) {
+        chunk_in[k] = cur;
+        const WideMap c = widen(maps[k]);
+        const unsigned long long e = c.e[cur >> 62];
+        cur = (e & ~((1ull << 62) - 1ull)) | ((cur & ((1ull << 62) - 1ull)) + (e & ((1ull << 62) - 1ull)));
+    }
+    if (t == kPpmCarryThreads - 1) misc->tokens = sScan[t].e[0] & ((1ull << 62) - 1ull);
+}
+
+// every chunk again from its entry state: token starts, each token walked
+template <typename Out>
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_parse(PpmText t, PpmMisc* __restrict__ misc,
+                                                           const unsigned long long* __restrict__ chunk_in,
+                                                           Out* __restrict__ out, unsigned long long nsamples,
+                                                           uint32_t maxval) {
+    __shared__ unsigned long long sWave[kPpmThreads / 64];
+    __shared__ __attribute__((aligned(16))) uint8_t sText[kPpmChunk + kPpmTail];
+    if (misc->flag == 0u) return;
+    const int tid = threadIdx.x;
+    uint32_t bad = 0, over = 0;
+    for (long long k = blockIdx.x; k < t.nch; k += gridDim.x) {
+        const long long c0 = k * kPpmChunk;
+        const long long pos = c0 + (long long)tid * kPpmWin;
+        PpmWin W;
+        ppm_window(t.text, pos, t.lo, t.len, t.safe, W);
+        reinterpret_cast<uint4*>(sText)[tid] = make_uint4(W.w[0], W.w[1], W.w[2], W.w[3]);
+        if (tid < kPpmTail / 4) {  // the tail: the first bytes of the next chunk
+            const long long p = c0 + kPpmChunk + 4 * tid;
+            uint32_t v = 0;
+            for (int j = 0; j < 4; ++j)
+                if (p + j < t.len) v |= (uint32_t)t.text[p + j] << (8 * j);
+            reinterpret_cast<uint32_t*>(sText + kPpmChunk)[tid] = v;
+        }
+        unsigned long long total;
+        const unsigned long long pre = ppm_block_scan(ppm_window_map(W), sWave, total);  // syncs sText too
+        const unsigned long long cin = chunk_in[k];
+        const int cs = (int)(cin >> 62);
+        const uint32_t e = (uint32_t)(pre >> (16 * cs)) & 0xFFFFu;
+        uint32_t starts;
+        (void)ppm_step(W, (int)(e >> 14), starts);
+        unsigned long long idx = (cin & ((1ull << 62) - 1ull)) + (e & 0x3FFFu);
+        while (starts) {
+            const int i = __builtin_ctz(starts);
+            starts &= starts - 1u;
+            bool ok;
+            const uint32_t v = parse_token_walk(t, sText, c0, pos + i, ok);
+            put_sample(out, idx++, nsamples, v, ok, maxval, bad, over);
+        }
+        __syncthreads();  // sText and sWave reused by the next chunk
+    }
+    if (bad) atomicOr(&misc->status, 1u);
+    if (over) atomicOr(&misc->status, 2u);
+}
+
+// ---------------------------------------------------------------- P6 samples
+// big-endian u16 samples -> host order (the extension's binary format; the range
+// check is the encoder's, as for dmmt_parse_ppm)
+__global__ __launch_bounds__(256) void k_ppm_swap16(const uint8_t* __restrict__ src, uint16_t* __restrict__ dst,
+                                                    unsigned long long n) {
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (unsigned long long)gridDim.x * blockDim.x)
+        dst[i] = (uint16_t)(((uint32_t)src[2 * i] << 8) | src[2 * i + 1]);
+}
+
+// ---------------------------------------------------------------- launchers
+static long long ppm_chunks(const uint8_t* text, size_t body_offset, size_t len, PpmText* t) {
+    const uintptr_t a = ((uintptr_t)text + body_offset) & ~(uintptr_t)15;
+    t->text = reinterpret_cast<const uint8_t*>(a);
+    t->lo = (long long)((uintptr_t)text + body_offset - a);
+    t->len = (long long)((uintptr_t)text + len - a);
+    t->safe = (long long)((intptr_t)(uintptr_t)text - (intptr_t)a);
+    t->nch = t->len > t->lo ? (t->len + kPpmChunk - 1) / kPpmChunk : 0;
+    return t->nch;
+}
+
+// chunks per carry row (a multiple of 4 for 16-byte loads of the counts)
+static long long ppm_row_chunks(long long nch) {
+    const long long r = (nch + kPpmCarryThreads - 1) / kPpmCarryThreads;
+    return (r + 3) / 4 * 4;
+}
+
+size_t ppm_counts_capacity(long long nch) { return (size_t)(ppm_row_chunks(nch) * kPpmCarryThreads + 16); }
+
+size_t ppm_chunk_count(const uint8_t* text, size_t body_offset, size_t len) {
+    PpmText t;
+    return (size_t)ppm_chunks(text, body_offset, len, &t);
+}
+
+hipError_t launch_ppm_p3(const uint8_t* text, size_t body_offset, size_t len, unsigned long long* maps,
+                         unsigned long long* chunk_in, uint32_t* counts, void* misc, void* out, int sample_bytes,
+                         unsigned long long nsamples, uint32_t maxval, hipStream_t st) {
+    PpmText t;
+    PpmMisc* m = reinterpret_cast<PpmMisc*>(misc);
+    hipError_t e = hipMemsetAsync(misc, 0, sizeof(PpmMisc), st);
+    if (e != hipSuccess || ppm_chunks(text, body_offset, len, &t) == 0) return e;
+    const unsigned nch = (unsigned)t.nch, gen = (unsigned)(t.nch < kPpmGeneralGrid ? t.nch : kPpmGeneralGrid);
+    // the comment-free kernels read at clamped addresses: texts of fewer than 32
+    // bytes go down the general path instead (flag preset)
+    const bool tiny = t.len - t.safe < 32;
+    if (tiny) {
+        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&m->flag), 1, 1, st)) != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(k_ppm_count, dim3(nch), dim3(kPpmThreads), 0, st, t, counts, m);
+    }
+    hipLaunchKernelGGL(k_ppm_maps, dim3(gen), dim3(kPpmThreads), 0, st, t, (const PpmMisc*)m, maps);
+    const long long rper = ppm_row_chunks(t.nch);
+    hipLaunchKernelGGL(k_ppm_carry, dim3(1), dim3(kPpmCarryThreads), 0, st, (const uint32_t*)counts,
+                       (const unsigned long long*)maps, t.nch, rper, m, chunk_in);
+    if (sample_bytes == 1) {
+        hipLaunchKernelGGL(k_ppm_fast<uint8_t>, dim3(nch), dim3(kPpmThreads), 0, st, t, m, (const uint32_t*)counts,
+                           (const unsigned long long*)chunk_in, rper, (uint8_t*)out, nsamples, maxval);
+        hipLaunchKernelGGL(k_ppm_parse<uint8_t>, dim3(gen), dim3(kPpmThreads), 0, st, t, m,
+                           (const unsigned long long*)chunk_in, (uint8_t*)out, nsamples, maxval);
+    } else {
+        hipLaunchKernelGGL(k_ppm_fast<uint16_t>, dim3(nch), dim3(kPpmThreads), 0, st, t, m, (const uint32_t*)counts,
+                           (const unsigned long long*)chunk_in, rper, (uint16_t*)out, nsamples, maxval);
+        hipLaunchKernelGGL(k_ppm_parse<uint16_t>, dim3(gen), dim3(kPpmThreads), 0, st, t, m,
+                           (const unsigned long long*)chunk_in, (uint16_t*)out, nsamples, maxval);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ppm_p6(const uint8_t* samples, void* out, int sample_bytes, unsigned long long nsamples,
+                         uint32_t, uint32_t*, hipStream_t st) {
+    if (nsamples == 0) return hipSuccess;
+    if (sample_bytes == 1) return hipMemcpyAsync(out, samples, nsamples, hipMemcpyDeviceToDevice, st);
+    const unsigned long long blocks = (nsamples + 255) / 256;
+    hipLaunchKernelGGL(k_ppm_swap16, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, st, samples,
+                       (uint16_t*)out, nsamples);
+    return hipGetLastError();
+}
+
+}  // namespace dmmt

@@ -90,6 +90,8 @@ def lib():
     L.dmmt_read_ppm.argtypes = [ctypes.c_char_p, P(DmmtImage)]
     L.dmmt_parse_ppm.argtypes = [vp, sz, P(DmmtImage)]
     L.dmmt_convert_ppm_to_jpeg.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, P(DmmtOptions)]
+    L.dmmt_parse_ppm_header.argtypes = [vp, sz, P(DmmtPpmHeader)]
+    L.dmmt_decode_ppm_device.argtypes = [vp, vp, sz, P(DmmtPpmHeader), vp, vp]
     L.dmmt_free.argtypes = [vp]
     L.dmmt_free.restype = None
     L.dmmt_strerror.argtypes = [ctypes.c_int]
@@ -148,6 +150,11 @@ class DmmtStripe(ctypes.Structure):
     _fields_ = [("d_rgb", ctypes.c_void_p), ("width", ctypes.c_uint16), ("height", ctypes.c_uint16),
                 ("maxval", ctypes.c_uint16), ("sample_bytes", ctypes.c_uint16), ("mcu_row0", ctypes.c_int32),
                 ("mcu_rows", ctypes.c_int32)]
+
+
+class DmmtPpmHeader(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint16), ("height", ctypes.c_uint16), ("maxval", ctypes.c_uint16),
+                ("binary", ctypes.c_int32), ("body_offset", ctypes.c_uint64)]
 
 
 STRIPE_HIST_WORDS = 2 * (16 + 256)
@@ -295,6 +302,16 @@ class PPMImageReader:
         return _image_from_c(im)
 
 
+def parse_ppm_header(data: bytes) -> DmmtPpmHeader:
+    """the four header tokens (ppm.rs:145-222) read on the host; body_offset is the
+    first byte after the whitespace that ended the max value"""
+    buf = ctypes.create_string_buffer(data, len(data))
+    h = DmmtPpmHeader()
+    _check(lib().dmmt_parse_ppm_header(ctypes.cast(buf, ctypes.c_void_p), len(data), ctypes.byref(h)),
+           "parse_ppm_header")
+    return h
+
+
 # ---------------------------------------------------------------- encoder
 
 class Encoder:
@@ -397,6 +414,30 @@ class Encoder:
 
     def synchronize(self):
         _check(lib().dmmt_ctx_synchronize(self._ctx), "synchronize")
+
+    def decode_ppm_device(self, d_text: int, length: int, header: DmmtPpmHeader, d_rgb: int, stream=None):
+        """parse_all_dots (ppm.rs:224-252) on the GPU: the whole file at d_text ->
+        width*height*3 samples at d_rgb (uint8 if maxval <= 255 else uint16)"""
+        _check(lib().dmmt_decode_ppm_device(self._ctx, d_text, length, ctypes.byref(header), d_rgb, stream),
+               "decode_ppm_device")
+
+    def read_ppm_device(self, data: bytes) -> Image:
+        """PPMImageReader::read_image with the body decoded on the GPU: header on the
+        host, file bytes to HBM, samples decoded there and copied back"""
+        h = parse_ppm_header(data)
+        n = h.width * h.height * 3
+        dt = np.uint8 if h.maxval <= 255 else np.uint16
+        d_text = self.malloc(max(len(data), 1))
+        d_rgb = self.malloc(max(n * np.dtype(dt).itemsize, 1))
+        try:
+            if data:
+                self.h2d(d_text, np.frombuffer(data, np.uint8))
+            self.decode_ppm_device(d_text, len(data), h, d_rgb)
+            arr = np.frombuffer(self.d2h(d_rgb, n * np.dtype(dt).itemsize), dt).reshape(h.height, h.width, 3)
+        finally:
+            self.free(d_text)
+            self.free(d_rgb)
+        return Image(h.width, h.height, h.maxval, arr.copy())
 
     def malloc(self, nbytes: int) -> int:
         p = ctypes.c_void_p()
@@ -623,13 +664,16 @@ def convert_ppm_to_jpeg(arguments: Arguments, encoder: Encoder | None = None) ->
             fout = open(arguments.output_file, "wb")
         except OSError as e:
             raise Error(-8, arguments.output_file) from e
-        with fout:
-            enc = encoder or Encoder(arguments.device)
-            image = PPMImageReader(fin).read_image()
-            opts = JpegTransformationOptions(arguments.chroma_subsampling_preset, arguments.bits_per_channel,
-                                             arguments.quantization_table_preset,
-                                             number_of_threads=arguments.number_of_threads)
-            JpegImageWriter(fout, image, opts, enc).write_image()
+        fout.close()
+    # read_image + write_image: the file's bytes go to the GPU as they are, its
+    # samples are decoded there (dmmt_decode_ppm_device) and encoded from HBM
+    enc = encoder or Encoder(arguments.device)
+    opts = JpegTransformationOptions(arguments.chroma_subsampling_preset, arguments.bits_per_channel,
+                                     arguments.quantization_table_preset,
+                                     number_of_threads=arguments.number_of_threads)
+    _check(lib().dmmt_convert_ppm_to_jpeg(enc.handle, os.fsencode(arguments.input_file),
+                                          os.fsencode(arguments.output_file), ctypes.byref(opts.to_c())),
+           "convert_ppm_to_jpeg")
 
 
 def encode_array(rgb, maxval: int = 255, subsampling: int = 2, luma=None, chroma=None, preset: int = 0,

@@ -36,13 +36,15 @@ def tokens(data: bytes):
 
 
 def _u16(tok, name):
-    try:
-        v = int(tok, 10)
-    except (TypeError, ValueError):
+    # Rust `str::parse::<u16>` (core::num from_str_radix): one optional leading '+',
+    # then at least one ASCII digit; no '-' for unsigned types; value <= 65535
+    digits = tok[1:] if tok.startswith("+") else tok
+    if not digits or any(c not in "0123456789" for c in digits):
         raise PPMError(f"ParsingOfTokenFailed({name})")
-    if not tok.isdigit() or v > 65535:
+    sig = digits.lstrip("0") or "0"  # leading zeros are accepted, however many
+    if len(sig) > 5 or int(sig) > 65535:
         raise PPMError(f"ParsingOfTokenFailed({name})")
-    return v
+    return int(sig)
 
 
 def read_p3(data: bytes):

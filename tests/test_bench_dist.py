@@ -68,7 +68,7 @@ def _worker(rank, world, port, out_dir):
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import bench
     log, lines = [], []
-    bench.main(["--gpus", str(world), "--steps", "20", "--warmup", "2", "--cpu-seconds", "0",
+    bench.main(["--gpus", str(world), "--steps", "20", "--warmup", "2", "--cpu-seconds", "0", "--ppm-steps", "0",
                 "--config", "1080p420q75x256"],
                make_encoder=lambda lr: StandInEncoder(lr, rank, log), emit=lines.append)
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:

@@ -1,0 +1,181 @@
+"""PPM ingest on the GPU (dmmt_decode_ppm_device): the P3 body
+decoded in HBM must give exactly the samples of the reference tokenizer/parser
+(ppm.rs:41-77, 224-252; restated by oracle/ppm.py and the host mirror
+dmmt_parse_ppm) and the same error variant, whatever the whitespace, comments
+(a '#' comment runs to its '\\n' and does not end a token), '+' signs, leading
+zeros, chunk boundaries (4096-byte chunks) and buffer alignment."""
+import os
+
+import numpy as np
+import pytest
+
+import dmmt_jpeg
+import oracle
+from conftest import GOLDEN, synthetic
+from oracle import ppm
+
+pytestmark = pytest.mark.gpu
+
+WS = [b" ", b"\n", b"\t", b"\r", b"\x0c"]
+
+
+def p3_text(rgb, maxval, rng, ws_max=3, comments=0.0, plus=0.0, zeros=0.0, header=b"P3\n"):
+    """a P3 file of rgb with random separators, comments, '+' signs, leading zeros"""
+    h, w, _ = rgb.shape
+    parts = [header, b"%d %d\n%d\n" % (w, h, maxval)]
+    for v in rgb.reshape(-1).tolist():
+        tok = b"%d" % v
+        if zeros and rng.random() < zeros:
+            tok = b"0" * int(rng.integers(1, 6)) + tok
+        if plus and rng.random() < plus:
+            tok = b"+" + tok
+        if comments and rng.random() < comments:  # a comment inside the token: does not split it
+            k = int(rng.integers(0, len(tok) + 1))
+            tok = tok[:k] + b"#c # x\n" + tok[k:]
+        parts.append(tok)
+        sep = b"".join(WS[int(i)] for i in rng.integers(0, len(WS), int(rng.integers(1, ws_max + 1))))
+        if comments and rng.random() < comments:
+            sep += b"# comment between tokens\n" + WS[int(rng.integers(0, len(WS)))]
+        parts.append(sep)
+    return b"".join(parts)
+
+
+def decode_gpu(encoder, data, align=0):
+    """the whole file at a device address with the given misalignment"""
+    h = dmmt_jpeg.parse_ppm_header(data)
+    n = h.width * h.height * 3
+    sb = 1 if h.maxval <= 255 else 2
+    d_text = encoder.malloc(len(data) + 64)
+    d_rgb = encoder.malloc(max(n * sb, 1))
+    try:
+        if data:
+            encoder.h2d(d_text + align, np.frombuffer(data, np.uint8))
+        encoder.decode_ppm_device(d_text + align, len(data), h, d_rgb)
+        return np.frombuffer(encoder.d2h(d_rgb, n * sb), np.uint8 if sb == 1 else np.uint16).reshape(
+            h.height, h.width, 3), h.maxval
+    finally:
+        encoder.free(d_text)
+        encoder.free(d_rgb)
+
+
+def host_code(data):
+    try:
+        dmmt_jpeg.PPMImageReader(data).read_image()
+        return 0
+    except dmmt_jpeg.Error as e:
+        return e.code
+
+
+def check_equal(encoder, data, align=0):
+    rgb, mx = ppm.read_p3(data)
+    got, gmx = decode_gpu(encoder, data, align)
+    assert gmx == mx
+    assert np.array_equal(got.astype(np.uint16), rgb)
+
+
+@pytest.mark.parametrize("name", ["16x16", "8x8", "7x17", "small"])
+def test_reference_fixtures(encoder, name):
+    check_equal(encoder, open(os.path.join(GOLDEN, name + ".ppm"), "rb").read())
+
+
+@pytest.mark.parametrize("w,h,ws_max,seed", [(37, 23, 1, 0), (160, 90, 3, 1), (300, 200, 8, 2), (1, 1, 1, 3)])
+def test_random_separators(encoder, w, h, ws_max, seed):
+    rng = np.random.default_rng(seed)
+    rgb = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+    for align in (0, 5):
+        check_equal(encoder, p3_text(rgb, 255, rng, ws_max=ws_max), align)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_comments_signs_leading_zeros(encoder, seed):
+    rng = np.random.default_rng(10 + seed)
+    rgb = rng.integers(0, 256, (61, 97, 3), dtype=np.uint8)
+    data = p3_text(rgb, 255, rng, comments=0.05, plus=0.05, zeros=0.05,
+                   header=b"P3 # a header comment\n# another\n")
+    for align in (0, 3, 15):
+        check_equal(encoder, data, align)
+
+
+def test_sixteen_bit_samples(encoder):
+    rng = np.random.default_rng(7)
+    rgb = rng.integers(0, 1001, (50, 70, 3), dtype=np.uint16)
+    check_equal(encoder, p3_text(rgb, 1000, rng, ws_max=2, comments=0.01))
+    rgb = rng.integers(0, 65536, (20, 30, 3), dtype=np.uint16)
+    check_equal(encoder, p3_text(rgb, 65535, rng))
+
+
+def test_long_runs_across_chunks(encoder):
+    """whitespace runs, comments and tokens longer than a chunk (4096 B) and its staged tail"""
+    rng = np.random.default_rng(5)
+    rgb = rng.integers(0, 256, (9, 11, 3), dtype=np.uint8)
+    parts = [b"P3\n11 9\n255\n"]
+    for i, v in enumerate(rgb.reshape(-1).tolist()):
+        if i % 37 == 0:
+            parts.append(b"0" * 5000 + b"%d" % v)           # a 5000-byte token
+        elif i % 41 == 0:
+            parts.append(b"%d#" % v + b"x" * 9000 + b"\n")  # a 9 KB comment before the separator
+        else:
+            parts.append(b"%d" % v)
+        parts.append(b" " * (6000 if i % 29 == 0 else 1))
+    data = b"".join(parts)
+    check_equal(encoder, data)
+    check_equal(encoder, data, 7)
+
+
+def test_synthetic_4k_frame(encoder):
+    """a whole 3840x2160 frame as P3 (~35 MB of text), as bench.py's ingest line"""
+    import bench
+    rgb = synthetic(3840, 2160)
+    data = bench.p3_bytes(rgb)
+    got, mx = decode_gpu(encoder, data)
+    assert mx == 255 and np.array_equal(got, rgb)
+
+
+@pytest.mark.parametrize("text", [
+    b"P3 1 1 255 0 0", b"P3 2 1 255 0 0 0", b"P3 1 1 255 0 0 0 1 1 1", b"P3 1 1 255 0 256 0",
+    b"P3 1 1 15 0 16 0", b"P3 1 1 255 0 0 -1", b"P3 1 1 255 0 + 1", b"P3 1 1 255 0 1a 1",
+    b"P3 1 1 255 0 65536 1", b"P3 1 1 255 0 0 1#x", b"P3 1 1 255 0 0 1 #x\n", b"P3 1 1 255 1 2 ++3",
+    b"P3 1 1 255 1 2 3 4 5", b"P3 2 1 255 1 2 3 4 5 x", b"P3 0 0 255", b"P3 0 0 255 ", b"P3 1 1 255",
+    b"P3 1 1 255\n1 2\xff 3", b"P3 2 2 255 " + b"1 " * 12 + b"# trailing comment"])
+def test_errors_match_host_reader(encoder, text):
+    code = host_code(text)
+    h = dmmt_jpeg.parse_ppm_header(text)
+    n = max(h.width * h.height * 3, 1)
+    d_text = encoder.malloc(len(text))
+    d_rgb = encoder.malloc(2 * n)
+    try:
+        encoder.h2d(d_text, np.frombuffer(text, np.uint8))
+        try:
+            encoder.decode_ppm_device(d_text, len(text), h, d_rgb)
+            got = 0
+        except dmmt_jpeg.Error as e:
+            got = e.code
+    finally:
+        encoder.free(d_text)
+        encoder.free(d_rgb)
+    assert got == code
+
+
+def test_p6_samples(encoder):
+    rgb = np.arange(3 * 5 * 7, dtype=np.uint8).reshape(5, 7, 3)
+    got, _ = decode_gpu(encoder, b"P6\n7 5\n255\n" + rgb.tobytes())
+    assert np.array_equal(got, rgb)
+    rgb16 = (np.arange(3 * 4 * 3, dtype=np.uint16) * 997).reshape(4, 3, 3)
+    got, _ = decode_gpu(encoder, b"P6 3 4 65535\n" + rgb16.astype(">u2").tobytes())
+    assert np.array_equal(got, rgb16)
+
+
+def test_convert_decodes_on_the_gpu(tmp_path, spec_tables):
+    """convert_ppm_to_jpeg: file bytes -> GPU decode -> GPU encode, byte-identical"""
+    rng = np.random.default_rng(3)
+    rgb = rng.integers(0, 256, (45, 67, 3), dtype=np.uint8)
+    src = tmp_path / "in.ppm"
+    src.write_bytes(p3_text(rgb, 255, rng, comments=0.02))
+    out = tmp_path / "o.jpg"
+    dmmt_jpeg.convert_ppm_to_jpeg(dmmt_jpeg.Arguments(str(src), str(out)))
+    assert out.read_bytes() == oracle.encode(rgb, 255, 2, *spec_tables)
+    bad = tmp_path / "bad.ppm"
+    bad.write_bytes(b"P3 2 2 255 1 2 3 4 5 6 7 8 9 10 11 x")
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        dmmt_jpeg.convert_ppm_to_jpeg(dmmt_jpeg.Arguments(str(bad), str(out)))
+    assert e.value.code == -2
