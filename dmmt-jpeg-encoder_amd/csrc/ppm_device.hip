@@ -8,22 +8,22 @@
 // \r) ends a token; every token must parse as a u16 (Rust `str::parse::<u16>`:
 // an optional '+', then decimal digits, value <= 65535).
 //
-// The text is cut into chunks of 4096 bytes (256 threads x 16 bytes).  What a
-// chunk does depends only on the state the text is in where it starts: inside a
-// comment or not, and whether the last kept (non-comment) byte before it was a
-// token byte.  Three launches:
-//  k_ppm_summary  every chunk's transition map: for each of the 4 entry states,
-//                 the exit state and the number of tokens starting in the chunk
-//                 (per thread from 16-bit byte-class masks, composed in order
-//                 over the workgroup)
-//  k_ppm_carry    one workgroup: ordered scan of the maps -> each chunk's entry
-//                 state and the index of its first token; the token count
-//  k_ppm_parse    every chunk again: token starts at its real entry state, each
-//                 token parsed by the thread it starts in (reading on past the
-//                 chunk when it must) and written at its index as u8 / u16;
-//                 parse errors and samples above maxval as status bits
-// A 16-byte window with no '#' (the normal case) is classified by mask
-// arithmetic; one with a '#' is walked byte by byte.
+// Two paths, chosen on the device (no host round trip):
+//  comment-free bodies (no '#' after the header: every P3 writer's output), 16 KB
+//  chunks, 64 bytes per thread, classified by SWAR word arithmetic --
+//   k_ppm_count  every chunk's token count (a token starts at each token byte
+//                after whitespace); raises the comment flag on any '#'
+//   k_ppm_carry  one workgroup: exclusive sums of the counts over 1024 rows
+//   k_ppm_fast   every chunk: its tokens parsed from registers (SWAR digits),
+//                staged in LDS in token order, stored coalesced
+//  bodies with comments (flag raised; otherwise these are empty launches), 4 KB
+//  chunks, 16 bytes per thread --
+//   k_ppm_maps   every chunk's transition map: for each of the 4 states the text
+//                can be in where the chunk starts (inside a comment?, last kept
+//                byte a token byte?) the state at its end and the tokens starting
+//                in it (window maps composed in order over the workgroup)
+//   k_ppm_carry  the ordered map scan: each chunk's entry state and first token
+//   k_ppm_parse  every chunk from its entry state, each token walked byte by byte
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -37,6 +37,8 @@ constexpr int kPpmThreads = 256;
 constexpr int kPpmChunk = kPpmWin * kPpmThreads;  // bytes per workgroup
 constexpr int kPpmTail = 256;                  // bytes staged past the chunk for tokens running on
 constexpr int kPpmCarryThreads = 1024;
+constexpr int kFastWin = 64;                        // comment-free path: bytes per thread
+constexpr int kFastChunk = kFastWin * kPpmThreads;  // and per workgroup
 
 // Transition maps: entry state s = (in comment) << 1 | (last kept byte a token
 // byte); entry s occupies bits [16s, 16s + 16): exit state << 14 | tokens started.
@@ -186,7 +188,8 @@ struct PpmText {
     const uint8_t* text;  // chunk 0 starts here (16-aligned)
     long long lo, len;    // body bytes [lo, len) relative to text
     long long safe;       // first byte of the caller's buffer relative to text (<= lo)
-    long long nch;
+    long long nch;        // general-path chunks (kPpmChunk bytes)
+    long long nfast;      // comment-free chunks (kFastChunk bytes)
 };
 
 // Comment-free bodies (no '#' after the header: every P3 writer's output) take a
@@ -204,44 +207,51 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t y) {
 // whitespace bytes of a word (char::is_ascii_whitespace), 4 bits: ' ' by a zero
 // test, 9 10 12 13 as the bytes in 8..15 whose low 3 bits select a 1 in an
 // 8-entry byte table (v_perm_b32)
-__device__ __forceinline__ uint32_t ws4(uint32_t x) {
+__device__ __forceinline__ uint32_t ws_hi(uint32_t x) {  // 0x80 in every whitespace byte
     const uint32_t sp = zero_bytes(x ^ 0x20202020u);
     const uint32_t in8 = zero_bytes((x & 0xF8F8F8F8u) ^ 0x08080808u);
     const uint32_t lk = __builtin_amdgcn_perm(0x00000101u, 0x00010100u, x & 0x07070707u);
-    const uint32_t h = sp | (in8 & (lk << 7));
-    return ((h >> 7) * 0x10204080u) >> 28;
+    return sp | (in8 & (lk << 7));
+}
+__device__ __forceinline__ uint32_t ws4(uint32_t x) {  // the same as 4 bits (shifts: no quarter-rate multiply)
+    const uint32_t h = ws_hi(x);
+    return ((h >> 7) & 1u) | ((h >> 14) & 2u) | ((h >> 21) & 4u) | (h >> 28);
 }
 
-// A window for the comment-free path: its words, valid bytes, whitespace and
-// whether it holds a '#'
-// whether it holds a '#'.  Lane 0 also reads the byte before the window and lane
-// 63 the 4 bytes after it (their neighbours' windows are in other waves), all
-// loads issued together.
+// A thread's 64 bytes for the comment-free path: its words, valid bytes and
+// whitespace (bit i = byte i), and whether it holds a '#'.  Lane 0 also reads the
+// byte before the window and lane 63 the 4 bytes after it (their neighbours'
+// windows are in other waves).  All loads are unconditional, at clamped addresses
+// inside the caller's buffer (the launcher guarantees t.len - t.safe >= 96), so
+// they are in flight together; windows at the ends of the body are fixed up
+// byte-wise.
 struct FastWin {
-    uint32_t w[4];
-    uint32_t valid, ws;
+    uint32_t w[16];
+    unsigned long long valid, ws;
     bool hash;
-    uint32_t prev_sig;   // lane 0: the byte before the window is a token byte
-    uint32_t next_w;     // lane 63: the 4 bytes after the window (0 past the text)
-    uint32_t next_end;   // lane 63: which of them end a token (whitespace, past the text)
+    uint32_t prev_sig;  // lane 0: the byte before the window is a token byte
+    uint32_t next_w;    // lane 63: the 4 bytes after the window (0 past the text)
+    uint32_t next_end;  // lane 63: which of them end a token (whitespace, past the text)
 };
 
 __device__ __forceinline__ void fast_window(const PpmText& t, long long pos, FastWin& F, bool want_next) {
-    // Unconditional loads at clamped addresses (inside the caller's buffer: the
-    // launcher guarantees t.len - t.safe >= 32), so all of them are in flight
-    // together; the few windows at the ends of the body are fixed up byte-wise.
     const int lane = lane_id();
     const long long s16 = (t.safe + 15) & ~15ll;
-    const bool full = pos >= t.safe && pos + kPpmWin <= t.len;
-    const uint4 v = *reinterpret_cast<const uint4*>(t.text + (full ? pos : s16));
-    const long long qp = min(max(pos - 1, t.lo), t.len - 1);
-    const uint32_t pb = t.text[qp];
-    const long long qn = pos + kPpmWin, qn4 = min(qn, (t.len - 4) & ~3ll);
-    const uint32_t nw = want_next ? *reinterpret_cast<const uint32_t*>(t.text + qn4) : 0u;
-    F.w[0] = full ? v.x : 0u;
-    F.w[1] = full ? v.y : 0u;
-    F.w[2] = full ? v.z : 0u;
-    F.w[3] = full ? v.w : 0u;
+    const bool full = pos >= t.safe && pos + kFastWin <= t.len;
+    const uint4* src = reinterpret_cast<const uint4*>(t.text + (full ? pos : s16));
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = src[q];
+    const uint32_t pb = t.text[min(max(pos - 1, t.lo), t.len - 1)];
+    const long long qn = pos + kFastWin;
+    const uint32_t nw = want_next ? *reinterpret_cast<const uint32_t*>(t.text + min(qn, (t.len - 4) & ~3ll)) : 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        F.w[4 * q] = full ? v[q].x : 0u;
+        F.w[4 * q + 1] = full ? v[q].y : 0u;
+        F.w[4 * q + 2] = full ? v[q].z : 0u;
+        F.w[4 * q + 3] = full ? v[q].w : 0u;
+    }
     F.prev_sig = (lane == 0 && pos - 1 >= t.lo && pos - 1 < t.len) ? (uint32_t)!ppm_ws(pb) : 0u;
     F.next_w = 0u;
     F.next_end = 0xFu;
@@ -256,51 +266,51 @@ __device__ __forceinline__ void fast_window(const PpmText& t, long long pos, Fas
             F.next_end = (ws4(F.next_w) | ~((1u << (int)in) - 1u)) & 0xFu;
         }
     }
-    F.valid = F.ws = 0u;
+    F.valid = F.ws = 0ull;
     F.hash = false;
-    if (pos + kPpmWin <= t.lo || pos >= t.len) return;
+    if (pos + kFastWin <= t.lo || pos >= t.len) return;
     if (!full) {
-        for (int k = 0; k < kPpmWin; ++k)
+        for (int k = 0; k < kFastWin; ++k)
             if (pos + k >= t.lo && pos + k < t.len) F.w[k >> 2] |= (uint32_t)t.text[pos + k] << (8 * (k & 3));
     }
-    const long long a = t.lo > pos ? t.lo - pos : 0, b = t.len - pos < kPpmWin ? t.len - pos : kPpmWin;
-    F.valid = ((1u << (int)b) - 1u) & ~((1u << (int)a) - 1u);
-    uint32_t ws = 0, hz = 0;
+    const long long a = t.lo > pos ? t.lo - pos : 0, b = t.len - pos < kFastWin ? t.len - pos : kFastWin;
+    F.valid = (b == 64 ? ~0ull : (1ull << (int)b) - 1ull) & ~((1ull << (int)a) - 1ull);
+    unsigned long long ws = 0;
+    uint32_t hz = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        ws |= ws4(F.w[k]) << (4 * k);
+    for (int k = 0; k < 16; ++k) {
+        ws |= (unsigned long long)ws4(F.w[k]) << (4 * k);
         hz |= zero_bytes(F.w[k] ^ 0x23232323u);
     }
     F.ws = ws & F.valid;
     F.hash = hz != 0u;  // (bytes outside the text are 0, never '#')
 }
 
-// this window's token starts when there are no comments: the previous byte is
+// the window's token starts when there are no comments: the previous byte is
 // the previous thread's last (a shuffle) or, for lane 0, read back
-__device__ __forceinline__ uint32_t fast_starts(const FastWin& W) {
-    const uint32_t sig = W.valid & ~W.ws;
-    uint32_t prev = (uint32_t)__shfl_up((int)((sig >> 15) & 1u), 1, 64);
+__device__ __forceinline__ unsigned long long fast_starts(const FastWin& W) {
+    const unsigned long long sig = W.valid & ~W.ws;
+    uint32_t prev = (uint32_t)__shfl_up((int)(uint32_t)(sig >> 63), 1, 64);
     if (lane_id() == 0) prev = W.prev_sig;
     return sig & ~((sig << 1) | prev);
 }
 
-
 // ---------------------------------------------------------------- comment-free path
-// Bodies without '#' (every P3 writer's output) in two passes over the text:
+// Bodies without '#' (every P3 writer's output) in two passes over the text,
+// 16 KB chunks (64 bytes per thread):
 //  k_ppm_count   each chunk's token count (a token starts at every token byte
 //                after whitespace); raises `flag` on any '#'
-//  k_ppm_carry   one workgroup: exclusive sum of the counts (or, with comments,
-//                the transition-map scan of the general path)
-//  k_ppm_fast    each chunk: its tokens parsed from registers -- a token of at
-//                most 4 bytes read with one byte-align from the window's words
-//                (and the next window's first word), digits checked and combined
-//                per byte lane (SWAR); longer ones, '+' and bad tokens take the
-//                byte walk -- staged in LDS in token order and stored coalesced
+//  k_ppm_carry   one workgroup: exclusive sums of the counts over 1024 rows of
+//                chunks (or, with comments, the transition-map scan of the
+//                general path)
+//  k_ppm_fast    each chunk: its row's base plus the counts before it in the row,
+//                then its tokens parsed from registers -- walking the window word
+//                by word, a token of at most 4 bytes is one byte-align of two
+//                words, its digits checked and combined per byte lane (SWAR);
+//                longer ones, '+' and bad tokens take the byte walk -- staged in
+//                LDS in token order and stored coalesced
 // With a '#' anywhere these write nothing that is used: the general kernels
 // (k_ppm_maps, k_ppm_parse) redo the body.
-__device__ __forceinline__ uint32_t pick5(const uint32_t (&w)[5], int j) {
-    return j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : j == 3 ? w[3] : w[4];
-}
 
 // A token from byte p (a token start) to the next kept whitespace, as
 // `str::parse::<u16>` (ppm.rs:247-251): the general byte walk, comments included.
@@ -344,24 +354,22 @@ __device__ __forceinline__ void put_sample(Out* out, unsigned long long idx, uns
     if (idx < nsamples) out[idx] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
 }
 
-
-
 // misc words (zeroed per call): status of the general path, status of the fast
-// path, token count, comment flag, chunk ticket
+// path, token count, comment flag
 struct PpmMisc {
     uint32_t status, status_fast;
     unsigned long long tokens;
-    uint32_t flag, ticket;
+    uint32_t flag, pad;
 };
 
 __global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* __restrict__ counts,
                                                            PpmMisc* __restrict__ misc) {
     __shared__ uint32_t sRed[kPpmThreads / 64];
     const int tid = threadIdx.x;
-    const long long pos = (long long)blockIdx.x * kPpmChunk + (long long)tid * kPpmWin;
+    const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
     FastWin F;
     fast_window(t, pos, F, false);
-    const uint32_t n = wave_sum_u32((uint32_t)__popc(fast_starts(F)));
+    const uint32_t n = wave_sum_u32((uint32_t)__popcll(fast_starts(F)));
     if (lane_id() == 0) sRed[tid >> 6] = n;
     const bool hash = __syncthreads_or(F.hash) != 0;
     if (tid == 0) {
@@ -372,6 +380,23 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* 
     }
 }
 
+// The token starting at byte i = 4j + r of a thread's window (lo, hi: words j
+// and j+1; e8: which of bytes 4j .. 4j+7 end a token): at most 4 digits by SWAR
+// -- one byte-align, digits checked per byte lane and combined with 24-bit
+// multiplies -- else ok = false and the caller walks it.
+__device__ __forceinline__ uint32_t fast_token(int r, uint32_t lo, uint32_t hi, uint32_t e8, bool& ok) {
+    const uint32_t e = (e8 >> r) & 0x1Fu;
+    const uint32_t L = e ? (uint32_t)__builtin_ctz(e) : 5u;
+    const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)r);
+    const uint32_t m = L >= 4 ? 0xFFFFFFFFu : (1u << (8 * L)) - 1u;
+    const uint32_t ge30 = ((x | 0x80808080u) - 0x30303030u) & 0x80808080u;
+    const uint32_t ge3a = ((x & 0x7F7F7F7Fu) + 0x46464646u) & 0x80808080u;
+    ok = L <= 4 && (((~ge30 | ge3a | x) & 0x80808080u) & m) == 0u;
+    const uint32_t d = (x & 0x0F0F0F0Fu & m) << (8 * (4 - min(L, 4u)));  // leading zero digits
+    const uint32_t t1 = __umul24(d & 0x00FF00FFu, 10u) + ((d >> 8) & 0x00FF00FFu);
+    return __umul24(t1 & 0xFFFFu, 100u) + (t1 >> 16);
+}
+
 template <typename Out>
 __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __restrict__ misc,
                                                           const uint32_t* __restrict__ counts,
@@ -380,37 +405,36 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
                                                           unsigned long long nsamples, uint32_t maxval) {
     __shared__ uint32_t sWave[kPpmThreads / 64];
     __shared__ unsigned long long sBase;
-    __shared__ Out sOut[kPpmChunk / 2];  // at most one token per two bytes
+    __shared__ Out sOut[kFastChunk / 2];  // at most one token per two bytes
     if (misc->flag != 0u) return;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const long long pos = (long long)blockIdx.x * kPpmChunk + (long long)tid * kPpmWin;
-    // the first token's index: the counts before this chunk within its carry row
-    // (wave 0, loads issued beside the window's)
+    const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
+    // the first token's index: the row's base + the counts before this chunk in
+    // its row (wave 0; loads issued beside the window's)
     const long long row0 = (long long)(blockIdx.x / per) * per, bx = (long long)blockIdx.x;
     FastWin F;
     fast_window(t, pos, F, true);
     const uint32_t c0 = counts[min(row0 + lane, bx)];
     uint32_t cnt = row0 + lane < bx ? c0 : 0u;
-    for (long long r0 = row0 + 64; r0 < bx; r0 += 64) {  // rows of more than 64 chunks (texts > 256 MB)
+    for (long long r0 = row0 + 64; r0 < bx; r0 += 64) {  // rows of more than 64 chunks (texts > 1 GB)
         const uint32_t c = counts[min(r0 + lane, bx)];
         cnt += r0 + lane < bx ? c : 0u;
     }
-    uint32_t starts = fast_starts(F);
-    const uint32_t n = (uint32_t)__popc(starts);
-    const uint32_t end16 = (F.ws | ~F.valid) & 0xFFFFu;  // bytes that end a token
-    uint32_t w[5] = {F.w[0], F.w[1], F.w[2], F.w[3], (uint32_t)__shfl_down((int)F.w[0], 1, 64)};
-    uint32_t next4 = (uint32_t)__shfl_down((int)end16, 1, 64) & 0xFu;
+    const unsigned long long starts = fast_starts(F);
+    const uint32_t n = (uint32_t)__popcll(starts);
+    const unsigned long long ends = F.ws | ~F.valid;  // bytes that end a token
+    uint32_t wn = (uint32_t)__shfl_down((int)F.w[0], 1, 64);
+    uint32_t next4 = (uint32_t)__shfl_down((int)(uint32_t)(ends & 0xFull), 1, 64) & 0xFu;
     if (lane == 63) {  // the next window belongs to the next wave (or chunk)
-        w[4] = F.next_w;
+        wn = F.next_w;
         next4 = F.next_end;
     }
-    const uint32_t ends = end16 | (next4 << 16);
+    const uint32_t inc = wave_incl_scan_u32(n);
+    if (lane == 63) sWave[wave] = inc;
     if (wave == 0) {
         cnt = wave_sum_u32(cnt);
         if (lane == 0) sBase = row_base[blockIdx.x / per] + cnt;
     }
-    const uint32_t inc = wave_incl_scan_u32(n);
-    if (lane == 63) sWave[wave] = inc;
     __syncthreads();
     uint32_t slot = inc - n, total = 0;
     for (int q = 0; q < kPpmThreads / 64; ++q) {
@@ -418,30 +442,23 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
         total += sWave[q];
     }
     uint32_t bad = 0, over = 0;
-    while (starts) {
-        const int i = __builtin_ctz(starts);
-        starts &= starts - 1u;
-        const uint32_t e = ends >> i;
-        const int L = (e & 0x1Fu) ? __builtin_ctz(e) : 5;
-        uint32_t v = 0;
-        bool ok = false;
-        if (L <= 4) {
-            const int j = i >> 2;
-            const uint32_t x = __builtin_amdgcn_alignbyte(pick5(w, j + 1), pick5(w, j), (uint32_t)(i & 3));
-            const uint32_t m = L == 4 ? 0xFFFFFFFFu : (1u << (8 * L)) - 1u;
-            const uint32_t ge30 = ((x | 0x80808080u) - 0x30303030u) & 0x80808080u;
-            const uint32_t ge3a = ((x & 0x7F7F7F7Fu) + 0x46464646u) & 0x80808080u;
-            ok = (((~ge30 | ge3a | x) & 0x80808080u) & m) == 0u;
-            if (ok) {
-                const uint32_t d = (x & 0x0F0F0F0Fu & m) << (8 * (4 - L));  // leading zero digits
-                const uint32_t t1 = (d & 0x00FF00FFu) * 10u + ((d >> 8) & 0x00FF00FFu);
-                v = (t1 & 0xFFFFu) * 100u + (t1 >> 16);
-            }
-        }
-        if (!ok) v = parse_token_walk(t, nullptr, 0, pos + i, ok);  // '+', long, or not a number
-        bad |= !ok;
-        over |= ok && v > maxval;
-        sOut[slot++] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {  // word by word: every register index is static
+        uint32_t sj = (uint32_t)(starts >> (4 * j)) & 0xFu;
+        if (!sj) continue;
+        const uint32_t lo = F.w[j], hi = j < 15 ? F.w[j + 1] : wn;
+        const uint32_t e8 = j < 15 ? (uint32_t)(ends >> (4 * j)) & 0xFFu
+                                   : ((uint32_t)(ends >> 60) & 0xFu) | (next4 << 4);
+        do {  // at most two tokens start in one word
+            const int r = __builtin_ctz(sj);
+            sj &= sj - 1u;
+            bool ok;
+            uint32_t v = fast_token(r, lo, hi, e8, ok);
+            if (!ok) v = parse_token_walk(t, nullptr, 0, pos + 4 * j + r, ok);  // '+', long, not a number
+            bad |= !ok;
+            over |= ok && v > maxval;
+            sOut[slot++] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+        } while (sj);
     }
     __syncthreads();
     const unsigned long long base = sBase;
@@ -510,7 +527,7 @@ __device__ __forceinline__ WideMap widen(unsigned long long m) {
 // chunk_in[k] = entry state << 62 | index of the chunk's first token; the token count
 __global__ __launch_bounds__(kPpmCarryThreads) void k_ppm_carry(const uint32_t* __restrict__ counts,
                                                                 const unsigned long long* __restrict__ maps,
-                                                                long long nch, long long rper,
+                                                                long long nch, long long nfast, long long rper,
                                                                 PpmMisc* __restrict__ misc,
                                                                 unsigned long long* __restrict__ chunk_in) {
     __shared__ WideMap sScan[kPpmCarryThreads];
@@ -531,8 +548,8 @@ __global__ __launch_bounds__(kPpmCarryThreads) void k_ppm_carry(const uint32_t* 
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const long long k = kb + 4 * u;
-                s += (k < nch ? c[u].x : 0u) + (k + 1 < nch ? c[u].y : 0u) + (k + 2 < nch ? c[u].z : 0u) +
-                     (k + 3 < nch ? c[u].w : 0u);
+                s += (k < nfast ? c[u].x : 0u) + (k + 1 < nfast ? c[u].y : 0u) + (k + 2 < nfast ? c[u].z : 0u) +
+                     (k + 3 < nfast ? c[u].w : 0u);
                 if (kb + 4 * u + 4 >= r0 + rper) break;
             }
         }
@@ -630,6 +647,7 @@ static long long ppm_chunks(const uint8_t* text, size_t body_offset, size_t len,
     t->len = (long long)((uintptr_t)text + len - a);
     t->safe = (long long)((intptr_t)(uintptr_t)text - (intptr_t)a);
     t->nch = t->len > t->lo ? (t->len + kPpmChunk - 1) / kPpmChunk : 0;
+    t->nfast = t->len > t->lo ? (t->len + kFastChunk - 1) / kFastChunk : 0;
     return t->nch;
 }
 
@@ -653,27 +671,32 @@ hipError_t launch_ppm_p3(const uint8_t* text, size_t body_offset, size_t len, un
     PpmMisc* m = reinterpret_cast<PpmMisc*>(misc);
     hipError_t e = hipMemsetAsync(misc, 0, sizeof(PpmMisc), st);
     if (e != hipSuccess || ppm_chunks(text, body_offset, len, &t) == 0) return e;
-    const unsigned nch = (unsigned)t.nch, gen = (unsigned)(t.nch < kPpmGeneralGrid ? t.nch : kPpmGeneralGrid);
-    // the comment-free kernels read at clamped addresses: texts of fewer than 32
+    const unsigned gen = (unsigned)(t.nch < kPpmGeneralGrid ? t.nch : kPpmGeneralGrid);
+    const unsigned nfast = (unsigned)t.nfast;
+    const long long rper = ppm_row_chunks(t.nfast);
+    // the comment-free kernels read at clamped addresses: texts of fewer than 96
     // bytes go down the general path instead (flag preset)
-    const bool tiny = t.len - t.safe < 32;
+    const bool tiny = t.len - t.safe < 96;
     if (tiny) {
         if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&m->flag), 1, 1, st)) != hipSuccess) return e;
     } else {
-        hipLaunchKernelGGL(k_ppm_count, dim3(nch), dim3(kPpmThreads), 0, st, t, counts, m);
+        hipLaunchKernelGGL(k_ppm_count, dim3(nfast), dim3(kPpmThreads), 0, st, t, counts, m);
     }
     hipLaunchKernelGGL(k_ppm_maps, dim3(gen), dim3(kPpmThreads), 0, st, t, (const PpmMisc*)m, maps);
-    const long long rper = ppm_row_chunks(t.nch);
     hipLaunchKernelGGL(k_ppm_carry, dim3(1), dim3(kPpmCarryThreads), 0, st, (const uint32_t*)counts,
-                       (const unsigned long long*)maps, t.nch, rper, m, chunk_in);
+                       (const unsigned long long*)maps, t.nch, t.nfast, rper, m, chunk_in);
     if (sample_bytes == 1) {
-        hipLaunchKernelGGL(k_ppm_fast<uint8_t>, dim3(nch), dim3(kPpmThreads), 0, st, t, m, (const uint32_t*)counts,
-                           (const unsigned long long*)chunk_in, rper, (uint8_t*)out, nsamples, maxval);
+        if (!tiny)
+            hipLaunchKernelGGL(k_ppm_fast<uint8_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, m,
+                               (const uint32_t*)counts, (const unsigned long long*)chunk_in, rper, (uint8_t*)out,
+                               nsamples, maxval);
         hipLaunchKernelGGL(k_ppm_parse<uint8_t>, dim3(gen), dim3(kPpmThreads), 0, st, t, m,
                            (const unsigned long long*)chunk_in, (uint8_t*)out, nsamples, maxval);
     } else {
-        hipLaunchKernelGGL(k_ppm_fast<uint16_t>, dim3(nch), dim3(kPpmThreads), 0, st, t, m, (const uint32_t*)counts,
-                           (const unsigned long long*)chunk_in, rper, (uint16_t*)out, nsamples, maxval);
+        if (!tiny)
+            hipLaunchKernelGGL(k_ppm_fast<uint16_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, m,
+                               (const uint32_t*)counts, (const unsigned long long*)chunk_in, rper, (uint16_t*)out,
+                               nsamples, maxval);
         hipLaunchKernelGGL(k_ppm_parse<uint16_t>, dim3(gen), dim3(kPpmThreads), 0, st, t, m,
                            (const unsigned long long*)chunk_in, (uint16_t*)out, nsamples, maxval);
     }
