@@ -167,3 +167,24 @@ def test_stripe_seam_composition():
             tail = whole[b + lens[k]:b + lens[k] + 16]
             assert nb == len(tail)
             assert nx == (int((tail + "0" * 16)[:16], 2) if tail else 0)
+
+
+@pytest.mark.parametrize("text,w,h,mx,binary,off", [
+    (b"P3\n2 1\n255\n1 2 3 4 5 6", 2, 1, 255, 0, 11),
+    (b"P3 # c\n2 1 # d 9\n255 1", 2, 1, 255, 0, 21),   # comments swallowed with their newline
+    (b"P3 2 1 25#x\n5 1", 2, 1, 255, 0, 14),           # a comment inside the max value token
+    (b"P6\n3 4\n65535\n", 3, 4, 65535, 1, 13),
+    (b"P3 1 1 255", 1, 1, 255, 0, 10)])                # maxval ended by the end of the file
+def test_ppm_header(L, text, w, h, mx, binary, off):  # ppm.rs:145-222 on the host
+    hd = dmmt_jpeg.parse_ppm_header(text)
+    assert (hd.width, hd.height, hd.maxval, hd.binary, hd.body_offset) == (w, h, mx, binary, off)
+    if not binary:  # the body from body_offset holds exactly the reference tokenizer's sample tokens
+        toks = list(ppm.tokens(text))
+        assert list(ppm.tokens(text[off:])) == toks[4:]
+
+
+def test_ppm_header_errors(L):
+    for text, code in [(b"", -1), (b"P5 1 1 1", -1), (b"P3 1 1", -1), (b"P3 1 x 1", -2)]:
+        with pytest.raises(dmmt_jpeg.Error) as e:
+            dmmt_jpeg.parse_ppm_header(text)
+        assert e.value.code == code
