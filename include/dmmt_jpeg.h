@@ -222,7 +222,25 @@ void dmmt_default_options(dmmt_options* opt); /* cli.rs defaults: P420, 8 bit, S
  * Samples are returned raw (uint16) with their maxval; free img->rgb with dmmt_free. */
 int dmmt_read_ppm(const char* path, dmmt_image* img);
 int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img);
-/* convert_ppm_to_jpeg (lib.rs:59-77): read PPM, encode on the GPU, write the file. */
+/* PPM ingest on the GPU.  The header (ppm.rs:145-222
+ * parse_header .. parse_max_value) is read on the host from the file's first bytes;
+ * body_offset is the first byte after the whitespace that ended the max value. */
+typedef struct {
+    uint16_t width, height, maxval;
+    int32_t binary;       /* 0: P3, the reference's format; 1: P6 (extension) */
+    uint64_t body_offset;
+} dmmt_ppm_header;
+int dmmt_parse_ppm_header(const uint8_t* data, size_t len, dmmt_ppm_header* hdr);
+/* PPMParser::parse_all_dots + the checks after it (ppm.rs:165-175, 224-252; the
+ * RangeColorFormat panic of color.rs:63-65 for P3) on the GPU: d_text holds the whole
+ * file (len bytes, header included) in device memory; d_rgb receives width*height*3
+ * samples, uint8 when maxval <= 255 else uint16 -- the same image dmmt_parse_ppm
+ * returns, and the same error codes.  Enqueued on stream (NULL: the context's stream)
+ * and synchronised before returning. */
+int dmmt_decode_ppm_device(dmmt_ctx* ctx, const uint8_t* d_text, size_t len, const dmmt_ppm_header* hdr,
+                           void* d_rgb, void* stream);
+/* convert_ppm_to_jpeg (lib.rs:59-77): read the PPM file, decode its samples and encode
+ * them on the GPU (dmmt_decode_ppm_device, then the encode path), write the file. */
 int dmmt_convert_ppm_to_jpeg(dmmt_ctx* ctx, const char* input_path, const char* output_path,
                              const dmmt_options* opt);
 void dmmt_free(void* p);
