@@ -95,10 +95,14 @@ __device__ __forceinline__ int bit_length(uint32_t v) { return v ? 32 - __clz((i
 // categorize.rs:22-32 category of a value (|v| <= 32767 here)
 __device__ __forceinline__ int category_of(int v) { return bit_length((uint32_t)(v < 0 ? -v : v)); }
 
+// category_of for |v| < 2^24 in two instructions: the frexp exponent of the exact
+// f32 value is the bit length of |v| (0 for 0)
+__device__ __forceinline__ int category_fast(int v) { return __builtin_amdgcn_frexp_expf((float)v); }
+
 // categorize.rs:34-46: the `cat` low bits of the extra-bits pattern
 __device__ __forceinline__ uint32_t extra_bits(int v, int cat) {
-    uint32_t p = v > 0 ? (uint32_t)v : (uint32_t)(v - 1);
-    return cat ? (p & ((1u << cat) - 1u)) : 0u;
+    const uint32_t p = (uint32_t)(v + (v >> 31));  // v, or v - 1 for a negative v
+    return __builtin_amdgcn_ubfe(p, 0u, (uint32_t)cat);  // width 0 (cat 0) extracts nothing
 }
 
 // Relaxed agent-scope accesses for the look-back status words (gfx950: sc1 loads

@@ -114,22 +114,21 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
         sink(((e & 0xFFFFu) << cat) | extra_bits(dcd, cat), (int)(e >> 16) + cat);
     }
     const uint32_t z = actab[0xF0];
-    int run = 0;
+    int r16 = 0;  // 16 * (current zero run): (run & 15) << 4 is r16 & 0xF0
 #pragma unroll
     for (int k = 1; k < 64; ++k) {
         if (k > kmax) continue;  // (wave-uniform) every later position is zero in every lane
         const int v = coef_at(b, k);
         if (v != 0) {
-            for (int r = run >> 4; r > 0; --r) sink(z & 0xFFFFu, (int)(z >> 16));
-            const int cat = category_of(v);
-            const uint32_t e = actab[((run & 15) << 4) | cat];
+            for (int r = r16 >> 8; r > 0; --r) sink(z & 0xFFFFu, (int)(z >> 16));
+            const int cat = category_fast(v);
+            const uint32_t e = actab[(r16 & 0xF0) | cat];
             sink(((e & 0xFFFFu) << cat) | extra_bits(v, cat), (int)(e >> 16) + cat);
-            run = 0;
-        } else {
-            ++run;
+            r16 = -16;
         }
+        r16 += 16;
     }
-    if (run || kmax < 63) {
+    if (r16 || kmax < 63) {
         const uint32_t e = actab[0];  // EOB
         sink(e & 0xFFFFu, (int)(e >> 16));
     }
@@ -167,13 +166,16 @@ struct WindowSink {
             put((uint32_t)(acc >> nacc), first);
             first = false;
             ++w;
-            acc &= (1ull << nacc) - 1ull;
         }
     }
     __device__ __forceinline__ void finish() {
         if (nacc > 0) put((uint32_t)(acc << (32 - nacc)), true);
     }
 };
+
+// The sinks never clear the bits they have flushed: with at most 32 bits per
+// piece, bits above the pending ones are shifted past bit 31 of every word taken
+// from acc, so the truncation to 32 bits drops them.
 
 // Private block slots of k_emit: every thread writes its block's bits MSB-first
 // from bit 0 of its own slot (no sharing, plain stores), word i of thread t at
@@ -194,7 +196,6 @@ struct SlotSink {
             nacc -= 32;
             if (wi < kSlotWords) slot[wi * 256] = (uint32_t)(acc >> nacc);
             ++wi;
-            acc &= (1ull << nacc) - 1ull;
         }
     }
     __device__ __forceinline__ uint32_t finish() {

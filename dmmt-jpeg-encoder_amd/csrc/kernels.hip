@@ -500,7 +500,9 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 w[4 * i + 2] = u.z;
                 w[4 * i + 3] = u.w;
             }
-            int run = 0;
+            // r16 = 16 * (current zero run), so (run & 15) << 4 is r16 & 0xF0 and
+            // run >> 4 is r16 >> 8; ZRLs are summed in a register, counted once
+            int r16 = 0;
             if (half) {  // zeros after the last non-zero of positions 1..31
                 const uint4* lo = reinterpret_cast<const uint4*>(sCoef + blk * CS);
                 uint32_t nzm = 0;  // bit k: position k non-zero
@@ -516,24 +518,25 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                     }
                 }
                 nzm &= ~1u;  // not the DC
-                run = nzm ? 31 - (31 - __clz((int)nzm)) : 31;
+                r16 = 16 * (nzm ? 31 - (31 - __clz((int)nzm)) : 31);
             }
             uint32_t* h = sHist + ((blk % BPM) < NLUMA ? 0 : 256);
+            uint32_t zrl = 0;
 #pragma unroll
             for (int kk = 0; kk < 32; ++kk) {
                 if (kk == 0 && !half) continue;  // the DC
                 const int v = (kk & 1) ? ((int)w[kk >> 1] >> 16) : (int)(int16_t)(w[kk >> 1] & 0xFFFFu);
                 if (v != 0) {
-                    if (run >= 16) atomicAdd(&h[0xF0], (uint32_t)(run >> 4));
-                    atomicAdd(&h[((run & 15) << 4) | category_of(v)], 1u);
-                    run = 0;
-                } else {
-                    ++run;
+                    if (r16 >= 256) zrl += (uint32_t)(r16 >> 8);
+                    atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
+                    r16 = -16;
                 }
+                r16 += 16;
             }
+            if (zrl) atomicAdd(&h[0xF0], zrl);
             if (half) {
-                if (run) atomicAdd(&h[0], 1u);                 // EOB
-                lastnz[e0 + blk] = (uint8_t)(63 - run);  // k_emit groups its walks by this
+                if (r16) atomicAdd(&h[0], 1u);                     // EOB
+                lastnz[e0 + blk] = (uint8_t)(63 - (r16 >> 4));  // k_emit groups its walks by this
             }
         }
         __syncthreads();
