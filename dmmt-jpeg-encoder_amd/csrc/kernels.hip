@@ -99,35 +99,6 @@ __device__ __forceinline__ void quantize_col8(const float (&v)[8], const float* 
     for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
 }
 
-// quantize_col8 for integer samples, whose coefficients are bounded: the samples
-// normalise into [0, 1] (a larger one is an error, color.rs:63-65), so Y, Cb, Cr
-// lie in [-128, 128] and every FDCT output in [-2048, 2048] (DC = sum / 8, AC
-// at most (1/4) * 64 * 128), to within a few ulps.  With q >= 1, a = |d/q| <= 2049:
-// |d * (1/q) - fl(d/q)| <= 3 * 2^-24 * a < 2^-11, so outside 2^-10 of a half-integer
-// both round to the same integer, and as t is then no tie, rint (half to even)
-// is round half away from zero; the saturation of `as i16` cannot trigger.
-// Lanes near a half-integer (or NaN: maxval 0) take the division afterwards.
-__device__ __forceinline__ void quantize_col8_bounded(const float (&v)[8], const float* q, const float* rq,
-                                                      uint32_t (&out)[4]) {
-    int x[8];
-    bool slow = false;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const float t = v[r] * rq[8 * r];
-        slow |= !(fabsf(__builtin_amdgcn_fractf(fabsf(t)) - 0.5f) > 0x1p-10f);
-        x[r] = (int)__builtin_rintf(t);
-    }
-    if (slow) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const float t = v[r] * rq[8 * r];
-            if (!(fabsf(__builtin_amdgcn_fractf(fabsf(t)) - 0.5f) > 0x1p-10f)) x[r] = quantize(v[r], q[8 * r]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
-}
-
 // arai.rs:7-26 constants, f32 literals as written in the reference
 #define DMMT_A1 0.70710678118654752440f
 #define DMMT_A2 0.5411961f
@@ -135,8 +106,19 @@ __device__ __forceinline__ void quantize_col8_bounded(const float (&v)[8], const
 #define DMMT_A4 1.3065629f
 #define DMMT_A5 0.3826834f
 
-// arai.rs:29-92: 8-point AAN butterfly with the output scaling folded in
-__device__ __forceinline__ void arai8(float (&v)[8]) {
+// arai.rs:85-92 output scaling, by output index
+#define DMMT_S0 0.3535533f
+#define DMMT_S1 0.2548978f
+#define DMMT_S2 0.27059805f
+#define DMMT_S3 0.30067244f
+#define DMMT_S4 0.35355338f
+#define DMMT_S5 0.4499881f
+#define DMMT_S6 0.6532815f
+#define DMMT_S7 1.2814577f
+__constant__ float c_arai_scale[8] = {DMMT_S0, DMMT_S1, DMMT_S2, DMMT_S3, DMMT_S4, DMMT_S5, DMMT_S6, DMMT_S7};
+
+// arai.rs:29-84: 8-point AAN butterfly, output k before its scaling factor
+__device__ __forceinline__ void arai8_unscaled(float (&v)[8]) {
     const float v10 = v[0] + v[7], v11 = v[1] + v[6], v12 = v[2] + v[5], v13 = v[3] + v[4];
     const float v14 = v[3] - v[4], v15 = v[2] - v[5], v16 = v[1] - v[6], v17 = v[0] - v[7];
     const float v20 = v10 + v13, v21 = v11 + v12, v22 = v11 - v12, v23 = v10 - v13;
@@ -148,14 +130,62 @@ __device__ __forceinline__ void arai8(float (&v)[8]) {
     const float v46 = (v26 * DMMT_A4) - ((v26 + v24) * DMMT_A5);
     const float v52 = v42 + v23, v53 = v23 - v42, v55 = v45 + v17, v57 = v17 - v45;
     const float v64 = v44 + v57, v65 = v55 + v46, v66 = v55 - v46, v67 = v57 - v44;
-    v[0] = v30 * 0.3535533f;
-    v[4] = v31 * 0.35355338f;
-    v[2] = v52 * 0.27059805f;
-    v[6] = v53 * 0.6532815f;
-    v[5] = v64 * 0.4499881f;
-    v[1] = v65 * 0.2548978f;
-    v[7] = v66 * 1.2814577f;
-    v[3] = v67 * 0.30067244f;
+    v[0] = v30;
+    v[4] = v31;
+    v[2] = v52;
+    v[6] = v53;
+    v[5] = v64;
+    v[1] = v65;
+    v[7] = v66;
+    v[3] = v67;
+}
+
+// arai.rs:29-92: the butterfly with its output scaling
+__device__ __forceinline__ void arai8(float (&v)[8]) {
+    arai8_unscaled(v);
+    v[0] = v[0] * DMMT_S0;
+    v[1] = v[1] * DMMT_S1;
+    v[2] = v[2] * DMMT_S2;
+    v[3] = v[3] * DMMT_S3;
+    v[4] = v[4] * DMMT_S4;
+    v[5] = v[5] * DMMT_S5;
+    v[6] = v[6] * DMMT_S6;
+    v[7] = v[7] * DMMT_S7;
+}
+
+// Quantisation for integer samples, whose coefficients are bounded: the samples
+// normalise into [0, 1] (a larger one is an error, color.rs:63-65), so Y, Cb, Cr
+// lie in [-128, 128] and every FDCT output in [-2048, 2048] (DC = sum / 8, AC at
+// most (1/4) * 64 * 128), to within a few ulps; with q >= 1, |d/q| <= 2049 and
+// the saturation of `as i16` cannot trigger.
+// The column pass's output scaling is folded into the reciprocal: u = the
+// unscaled column outputs (arai8_unscaled), crq[8r] = fl(scale_r * fl(1/q)).
+// t = u * crq is within 5 * 2^-24 * 2049 < 2^-10 of the correctly rounded d/q,
+// d = fl(u * scale_r) (five roundings apart), so where t lies farther than 2^-10
+// from a half-integer -- |t - rint(t)| < 1/2 - 2^-10, the difference exact -- both
+// round to the same integer, and as t is then no tie, rint (half to even) is
+// round half away from zero.  The other lanes (and NaN: maxval 0, q 0) redo d and
+// the division afterwards.
+__device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const float* q, const float* crq,
+                                                     uint32_t (&out)[4]) {
+    int x[8];
+    bool slow = false;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const float t = u[r] * crq[8 * r];
+        const float n = __builtin_rintf(t);
+        slow |= !(fabsf(t - n) < 0.4990234375f);  // 1/2 - 2^-10
+        x[r] = (int)n;
+    }
+    if (slow) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float t = u[r] * crq[8 * r];
+            if (!(fabsf(t - __builtin_rintf(t)) < 0.4990234375f)) x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
 }
 
 // color.rs:75-100
@@ -280,7 +310,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     __shared__ uint32_t sHist[2 * 256];
     __shared__ float sLut[256];
     __shared__ float sQ[128];
-    __shared__ float sRQ[128];  // 1/q, correctly rounded
+    __shared__ float sRQ[128];  // 1/q, correctly rounded; integer samples: fl(scale_row * fl(1/q))
     int16_t* const sCoef = reinterpret_cast<int16_t*>(sT);
 
     DMMT_TRACE_START;
@@ -290,7 +320,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     const long long fbytes = (long long)g.width * g.height * 3 * SB;
     for (int i = tid; i < 512; i += 256) sHist[i] = 0;
     if (tid < 128) sQ[tid] = qtab[tid];
-    if (tid < 128) sRQ[tid] = 1.0f / qtab[tid];
+    if (tid < 128) sRQ[tid] = SB == 4 ? 1.0f / qtab[tid] : c_arai_scale[(tid >> 3) & 7] * (1.0f / qtab[tid]);
     if (SB == 1) sLut[tid] = norm_lut[tid];
     // the column pass always handles column tid & 7: its 8 zigzag destinations
     uint8_t zz[8];
@@ -441,12 +471,14 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 float v[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = sT[blk * BS + i * 8 + col];
-                arai8(v);
                 const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
-                if constexpr (SB == 4)  // Image<f32> dots: unbounded coefficients
+                if constexpr (SB == 4) {  // Image<f32> dots: unbounded coefficients
+                    arai8(v);
                     quantize_col8(v, q, rq, qv[jj]);
-                else
-                    quantize_col8_bounded(v, q, rq, qv[jj]);
+                } else {
+                    arai8_unscaled(v);
+                    quantize_col8_scaled(v, q, rq, qv[jj]);
+                }
             }
         }
         __syncthreads();  // every column read: the int16 image may now overwrite sT
