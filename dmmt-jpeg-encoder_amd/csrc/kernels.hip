@@ -307,7 +307,12 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     // row-transformed blocks (A..C), then the quantised int16 blocks (C..E)
     __shared__ __attribute__((aligned(16))) float sT[NB * BS];
     __shared__ __attribute__((aligned(16))) uint8_t sRaw[Raw::BYTES];
-    __shared__ uint32_t sHist[2 * 256];
+    // two copies of the AC symbol histograms (luma, chroma), for even and odd
+    // blocks: half the same-address collisions of the counting atomics (lanes of
+    // a wave often count the same symbol at the same position); 513 words apart,
+    // so a symbol's two counters sit in different banks
+    constexpr int HC = 2;
+    __shared__ uint32_t sHist[513 * HC];
     __shared__ float sLut[256];
     __shared__ float sQ[128];
     __shared__ float sRQ[128];  // 1/q, correctly rounded; integer samples: fl(scale_row * fl(1/q))
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     const int frame = blockIdx.y;
     const uint8_t* fbase = reinterpret_cast<const uint8_t*>(rgb + (size_t)frame * frame_stride);
     const long long fbytes = (long long)g.width * g.height * 3 * SB;
-    for (int i = tid; i < 512; i += 256) sHist[i] = 0;
+    for (int i = tid; i < 513 * HC; i += 256) sHist[i] = 0;
     if (tid < 128) sQ[tid] = qtab[tid];
     if (tid < 128) sRQ[tid] = SB == 4 ? 1.0f / qtab[tid] : c_arai_scale[(tid >> 3) & 7] * (1.0f / qtab[tid]);
     if (SB == 1) sLut[tid] = norm_lut[tid];
@@ -552,7 +557,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 nzm &= ~1u;  // not the DC
                 r16 = 16 * (nzm ? 31 - (31 - __clz((int)nzm)) : 31);
             }
-            uint32_t* h = sHist + ((blk % BPM) < NLUMA ? 0 : 256);
+            uint32_t* h = sHist + ((blk % BPM) < NLUMA ? 0 : 256) + 513 * (blk % HC);
             uint32_t zrl = 0;
 #pragma unroll
             for (int kk = 0; kk < 32; ++kk) {
@@ -578,7 +583,9 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     if (bad) atomicOr(status, 1);
     uint32_t* gh = ac_hist + ((size_t)frame * kHistReps + (blockIdx.x % kHistReps)) * 512;
     for (int i = tid; i < 512; i += 256) {
-        const uint32_t v = sHist[i];
+        uint32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < HC; ++c) v += sHist[513 * c + i];
         if (v) atomicAdd(&gh[i], v);
     }
     DMMT_TRACE(5);
