@@ -405,7 +405,10 @@ int take_status(dmmt_ctx* c, hipStream_t st) {
         HIP_TRY(hipMemsetAsync(c->status.p, 0, sizeof(int), st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    // in the reference's order: the sample range is checked when the PPM is read,
+    // categories while the blocks are categorised, symbols while they are written
     if (s & 1) return DMMT_E_VALUE_EXCEEDS_MAX;
+    if (s & 4) return DMMT_E_CATEGORY_RANGE;
     if (s & 2) return DMMT_E_HUFFMAN_SYMBOL_MISSING;
     if (s & 16) return DMMT_E_CAPACITY;
     return DMMT_OK;

@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 cbv[k] = cbs;
                 crv[k] = crs;
             }
-            bad |= (int)(smax > (uint32_t)g.maxval);
+            bad |= (int)(smax > (uint32_t)g.maxval);  // status bit 1
 #pragma unroll
             for (int dy = 0; dy < VR; ++dy) {
                 const int ly = r * VR + dy;
@@ -564,6 +564,9 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 if (kk == 0 && !half) continue;  // the DC
                 const int v = (kk & 1) ? ((int)w[kk >> 1] >> 16) : (int)(int16_t)(w[kk >> 1] & 0xFFFFu);
                 if (v != 0) {
+                    // Image<f32> dots only (integer samples bound |v| by 2049): -32768
+                    // has no category (categorize.rs:25-30)
+                    if (SB == 4 && v == -32768) bad |= 4;
                     if (r16 >= 256) zrl += (uint32_t)(r16 >> 8);
                     atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
                     r16 = -16;
@@ -580,7 +583,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
         DMMT_TRACE(4);
     }
 
-    if (bad) atomicOr(status, 1);
+    if (bad) atomicOr(status, bad);  // 1: sample above maxval, 4: category out of range
     uint32_t* gh = ac_hist + ((size_t)frame * kHistReps + (blockIdx.x % kHistReps)) * 512;
     for (int i = tid; i < 512; i += 256) {
         uint32_t v = 0;
@@ -596,13 +599,15 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
 // DC difference per component in emission order (categorize.rs:153-169), with
 // the predictor reset at restart-interval starts (extension), + DC histograms.
 __global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, int16_t* __restrict__ dcdiff, Geom g,
-                                                uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/) {
+                                                uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
+                                                int* __restrict__ status) {
     __shared__ uint32_t sH[32];
     const int tid = threadIdx.x;
     const int frame = blockIdx.y;
     if (tid < 32) sH[tid] = 0;
     __syncthreads();
     const long long base = (long long)frame * g.bpf;
+    bool bad = false;
     for (long long el = (long long)blockIdx.x * 256 + tid; el < g.bpf; el += (long long)gridDim.x * 256) {
         const int m = (int)(el / g.bpm);
         const int k = (int)(el - (long long)m * g.bpm);
@@ -615,9 +620,11 @@ __global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, 
         const int cur = dc[base + el];
         const int pv = prev >= 0 ? (int)dc[base + prev] : 0;
         const int16_t d = (int16_t)(cur - pv);  // i16 subtraction
+        bad |= d == -32768;                      // no category (categorize.rs:25-30)
         dcdiff[base + el] = d;
         atomicAdd(&sH[(k < g.n_luma ? 0 : 16) + category_of(d)], 1u);
     }
+    if (bad) atomicOr(status, 4);
     __syncthreads();
     if (tid < 32 && sH[tid]) atomicAdd(&dc_hist[((size_t)frame * kHistReps + blockIdx.x % kHistReps) * 32 + tid], sH[tid]);
 }
@@ -1022,7 +1029,8 @@ __global__ __launch_bounds__(256) void k_synthetic(uint8_t* __restrict__ rgb, in
 // DC values and AC histograms k_front would have produced are rebuilt here.
 namespace dmmt {
 __global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coef, Geom g, int16_t* __restrict__ dc,
-                                                 uint8_t* __restrict__ lastnz, uint32_t* __restrict__ ac_hist) {
+                                                 uint8_t* __restrict__ lastnz, uint32_t* __restrict__ ac_hist,
+                                                 int* __restrict__ status) {
     __shared__ uint32_t sHist[512];
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
@@ -1037,6 +1045,7 @@ __global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coe
             lastnz[base + el] = (uint8_t)(nz ? 63 - __clzll(nz) : 0);
         }
         const int t = (int)(el % g.bpm) < g.n_luma ? 0 : 1;
+        if (lane > 0 && c == -32768) atomicOr(status, 4);  // no category (categorize.rs:25-30)
         if (lane > 0 && c != 0) {
             const unsigned long long below = nz & ((1ull << lane) - 1ull);
             const int p = below ? 63 - __clzll(below) : 0;
@@ -1123,14 +1132,15 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 
 hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
     dim3 grid(clampi((g.bpf + 3) / 4, 1, 1024 / n_frames > 0 ? 1024 / n_frames : 1), n_frames);
-    hipLaunchKernelGGL(k_ac_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, g, w.dc, w.lastnz, w.ac_hist);
+    hipLaunchKernelGGL(k_ac_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, g, w.dc, w.lastnz, w.ac_hist,
+                       w.status);
     return hipGetLastError();
 }
 
 hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
     const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
-    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist);
+    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist, w.status);
     return hipGetLastError();
 }
 

@@ -134,6 +134,43 @@ def test_value_above_maxval_is_an_error(encoder, spec_tables):
     assert encoder.encode(dmmt_jpeg.Image.from_array(ok), opts(2, *spec_tables)) == oracle.encode(ok, 255, 2, *spec_tables)
 
 
+@pytest.mark.parametrize("where", ["ac", "dc", "dc_diff"])
+def test_category_out_of_range_is_an_error(encoder, spec_tables, where):
+    """categorize.rs:25-30 panics on -32768 (category 16): an AC coefficient, a
+    first-block DC (difference from predictor 0) or a DC difference that wraps
+    to -32768 in i16 -- the oracle's CategoryOutOfRange, as an error code here."""
+    blocks = np.zeros((3 * 4, 64), np.int16)  # 32x8 pixels, 4:4:4: 4 MCUs
+    if where == "ac":
+        blocks[4, 5] = -32768
+    elif where == "dc":
+        blocks[0, 0] = -32768
+    else:
+        blocks[0, 0], blocks[3, 0] = 16384, -16384  # luma DCs of MCUs 0, 1: -16384 - 16384 wraps
+    with pytest.raises(oracle.OracleError) as eo:
+        oracle.encode_coefficients(blocks, 32, 8, 0, *spec_tables)
+    assert eo.value.code == -101
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        encoder.encode_coefficients(blocks, 32, 8, opts(0, *spec_tables))
+    assert e.value.code == -101
+    # the context stays usable afterwards
+    ok = synthetic(16, 16)
+    assert encoder.encode(dmmt_jpeg.Image.from_array(ok), opts(0, *spec_tables)) == oracle.encode(ok, 255, 0, *spec_tables)
+
+
+def test_category_out_of_range_from_f32_dots(encoder, spec_tables):
+    """Image<f32> dots far outside [0, 1] saturate `as i16` (quantizer.rs:60) to
+    -32768, whose category the reference cannot encode (categorize.rs:25-30)."""
+    dots = np.full((8, 8, 3), -1000.0, np.float32)
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        encoder.encode(dmmt_jpeg.Image.from_array(dots, 255), opts(0, *spec_tables))
+    assert e.value.code == -101
+    dots[:, 4:, :] = 1000.0  # a saturated AC coefficient beside a finite DC
+    dots[:, :4, :] = -1000.0
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        encoder.encode(dmmt_jpeg.Image.from_array(dots, 255), opts(0, *spec_tables))
+    assert e.value.code == -101
+
+
 def test_bits_per_channel_written_to_sof(encoder, spec_tables):
     rgb = synthetic(24, 16)
     for bits in (8, 16, 32):
