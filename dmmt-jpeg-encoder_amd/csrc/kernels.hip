@@ -222,8 +222,30 @@ struct RawTile {
         return (int)(((uintptr_t)fbase + (uintptr_t)start) & 15u);
     }
 
+    // misalign() from 32-bit arithmetic: only the address's low 4 bits matter
+    __device__ static __forceinline__ int misalign32(const uint8_t* fbase, const Geom& g, int x0, int py) {
+        return (int)(((uint32_t)(uintptr_t)fbase + (uint32_t)(py * g.width + x0) * (uint32_t)(3 * sizeof(Sample))) & 15u);
+    }
+
     __device__ static __forceinline__ void load(const uint8_t* __restrict__ fbase, long long fbytes, const Geom& g,
                                                 int x0, int y0, int tid, uint4 (&v)[NQ]) {
+        // Interior tile (wave-uniform): every row inside the image, no pixel past its
+        // right edge, every chunk inside the frame's bytes -- plain aligned loads, no
+        // masking.  The bytes a chunk holds beyond the tile row are never read.
+        const long long last = row_start(g, x0, y0 + ROWS - 1);
+        if (x0 + 256 <= g.width && y0 + ROWS <= g.height && row_start(g, x0, y0) >= 16 && last + RB + 16 <= fbytes) {
+            const uint8_t* tb = fbase + row_start(g, x0, y0);
+            const uint32_t rowpitch = (uint32_t)g.width * (uint32_t)(3 * sizeof(Sample));
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) {
+                const int q = tid + 256 * i;
+                const int row = q / RC, j = q - (q / RC) * RC;
+                const uint8_t* r = tb + (size_t)((uint32_t)row * rowpitch);  // pointer arithmetic: stays global
+                const uint8_t* a = r - ((uint32_t)(uintptr_t)r & 15u) + 16u * (uint32_t)j;
+                v[i] = q < NCHUNK ? *reinterpret_cast<const uint4*>(a) : make_uint4(0u, 0u, 0u, 0u);
+            }
+            return;
+        }
         const long long rowbytes = (long long)min(256, g.width - x0) * 3 * (long long)sizeof(Sample);
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
@@ -367,8 +389,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
 #pragma unroll
             for (int dy = 0; dy < VR; ++dy) {
                 const int ly = r * VR + dy;
-                const long long start = Raw::row_start(g, x0, y0 + ly);
-                const int mis = Raw::misalign(fbase, start);
+                const int mis = Raw::misalign32(fbase, g, x0, y0 + ly);
                 const uint8_t* src = sRaw + ly * Raw::RS + mis + lx0 * 3 * SB;
                 fsrc[dy] = reinterpret_cast<const float*>(src);
                 if constexpr (SB == 4) {
