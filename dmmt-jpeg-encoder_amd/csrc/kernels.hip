@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "device_common.hpp"
 #include "jpeg_common.hpp"
 #include "kernels.hpp"
@@ -357,6 +359,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     const int tiles_per_row = (g.mcux + TM - 1) / TM;
     const int ntiles = tiles_per_row * g.mcuy;
     int bad = 0;
+    const bool check_range = SB != 4 && g.maxval < (SB == 1 ? 255 : 65535);
 
     uint4 raw[Raw::NQ];
     if ((int)blockIdx.x < ntiles) {
@@ -381,7 +384,10 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
 
         // ---- A: colour + subsampling + row pass (color.rs:75-100, padder.rs: outside
         //      = black, subsampling.rs Subsampler::rect x outer / y inner, arai.rs:97-99)
-        if (tid < NJ) {
+        // the range check (color.rs:63-65) only where a sample can exceed maxval:
+        // not for u8 samples with maxval 255 or u16 with 65535 (the PPM norm)
+        auto phase_a = [&](auto range_check) {
+            constexpr bool CHECK = decltype(range_check)::value;
             const int c = tid % CB, r = tid / CB;  // chroma block, chroma row
             const int lx0 = c * 8 * HR;            // first pixel column of the job
             uint32_t pw[VR][SB == 4 ? 1 : PXW];    // raw bytes of the job's VR pixel rows (integer samples)
@@ -432,7 +438,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                                 sv[ch] = SB == 1 ? (pw[dy][si >> 2] >> (8 * (si & 3))) & 0xFFu
                                                  : (pw[dy][si >> 1] >> (16 * (si & 1))) & 0xFFFFu;
                             }
-                            smax = max(smax, max(sv[0], max(sv[1], sv[2])));
+                            if constexpr (CHECK) smax = max(smax, max(sv[0], max(sv[1], sv[2])));
                             if (SB == 1) {
                                 rr = sLut[sv[0]];
                                 gg = sLut[sv[1]];
@@ -462,7 +468,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 cbv[k] = cbs;
                 crv[k] = crs;
             }
-            bad |= (int)(smax > (uint32_t)g.maxval);  // status bit 1
+            if constexpr (CHECK) bad |= (int)(smax > (uint32_t)g.maxval);  // status bit 1
 #pragma unroll
             for (int dy = 0; dy < VR; ++dy) {
                 const int ly = r * VR + dy;
@@ -482,6 +488,12 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
             float4* orr = reinterpret_cast<float4*>(sT + (NYB + CB + c) * BS + r * 8);
             orr[0] = make_float4(crv[0], crv[1], crv[2], crv[3]);
             orr[1] = make_float4(crv[4], crv[5], crv[6], crv[7]);
+        };
+        if (tid < NJ) {
+            if (check_range)
+                phase_a(std::integral_constant<bool, true>{});
+            else
+                phase_a(std::integral_constant<bool, false>{});
         }
         __syncthreads();
         DMMT_TRACE(0);
