@@ -57,22 +57,11 @@ __device__ __forceinline__ int16_t quantize(float d, float q) {
     return (int16_t)(int)x;
 }
 
-// The same result as quantize(d, q) without the division in the common case:
-// t = d * (1/q) is within 1.5 * 2^-23 |d/q| of the correctly rounded quotient, so
-// round(t) == round(fl(d/q)) unless t lies within that distance of a
-// half-integer (or is huge / not finite); only those lanes divide.
-__device__ __forceinline__ int16_t quantize_rcp(float d, float q, float rq) {
-    float t = d * rq;
-    const float a = fabsf(t);
-    if (!(a < 4194304.0f) || !(fabsf((a - floorf(a)) - 0.5f) > a * 0x1p-20f)) t = d / q;
-    float x = roundf(t);
-    if (x != x) return 0;
-    x = fminf(fmaxf(x, -32768.0f), 32767.0f);
-    return (int16_t)(int)x;
-}
-
-// quantize_rcp over the 8 rows of one column (row r scaled by q[8r], rq[8r] = 1/q):
-// branch-free on the fast path -- round half away from zero of a = |d * (1/q)| is
+// Image<f32> dots: quantize(d, q) over the 8 rows of one column (row r scaled by
+// q[8r], rq[8r] = 1/q) without the division in the common case, branch-free on
+// the fast path.  t = d * (1/q) is within 1.5 * 2^-23 * |t| of the correctly
+// rounded quotient, so both round alike unless t lies within a * 2^-20 of a
+// half-integer.  Round half away from zero of a = |t| is
 // trunc(a + 0.5) there, exactly: a < 2^22 and a's fraction is farther than
 // a * 2^-20 > ulp(a + 0.5) / 2 from 1/2, so the addition cannot round across an
 // integer -- and the rare lanes outside it redone with the division afterwards.
@@ -297,7 +286,7 @@ struct RawTile {
 //     block) converts its 8*HR x VR pixels (raw bytes from LDS), box-averages the
 //     chroma in the reference's sum order and runs the row pass of the HR*VR luma
 //     rows and the two chroma rows in registers -> block-major LDS (stride BS)
-//  C  column DCT + quantise (quantize_rcp): one lane per (block, column); results
+//  C  column DCT + quantise (quantize_col8_scaled): one lane per (block, column); results
 //     held in registers across a barrier, then scattered in zigzag order into the
 //     (aliased) int16 block image in local MCU emission order
 //  D  coalesced 16-byte stores of the tile's blocks + DC values (wave 3), beside
