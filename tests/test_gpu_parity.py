@@ -207,6 +207,40 @@ def test_device_resident_api_and_generator(encoder, spec_tables):
             encoder.free(p)
 
 
+@pytest.mark.parametrize("sub", SUBS)
+@pytest.mark.parametrize("sample_bytes", [1, 2])
+def test_device_frames_misaligned_interior_tiles(encoder, spec_tables, sub, sample_bytes):
+    """Frames packed at odd byte offsets, widths a multiple of the 256-pixel tile:
+    k_front's interior-tile loads (aligned 16-byte chunks, no masking) start a
+    chunk up to 15 bytes before a row and read the next tile's bytes; the first
+    and last tiles of each frame take the guarded path."""
+    w, h, n = 512, 24, 3
+    rng = np.random.default_rng(17 + sub)
+    maxval = 255 if sample_bytes == 1 else 1023
+    dt = np.uint8 if sample_bytes == 1 else np.uint16
+    frames = rng.integers(0, maxval + 1, (n, h, w, 3)).astype(dt)
+    fbytes = w * h * 3 * sample_bytes
+    stride = fbytes + 6 * sample_bytes  # every frame starts at a different residue mod 16
+    buf = np.zeros(stride * n + 16, np.uint8)
+    for f in range(n):
+        buf[3 * sample_bytes + f * stride:3 * sample_bytes + f * stride + fbytes] = frames[f].reshape(-1).view(np.uint8)
+    d_in = encoder.malloc(buf.nbytes)
+    ostride = dmmt_jpeg.max_jpeg_bytes(w, h, sub)
+    d_out = encoder.malloc(ostride * n)
+    d_len = encoder.malloc(4 * n)
+    try:
+        encoder.h2d(d_in, buf)
+        encoder.encode_device(d_in + 3 * sample_bytes, n, w, h, opts(sub, *spec_tables), d_out, ostride, d_len,
+                              frame_stride=stride, maxval=maxval, sample_bytes=sample_bytes)
+        encoder.synchronize()
+        lens = np.frombuffer(encoder.d2h(d_len, 4 * n), np.uint32)
+        for f in range(n):
+            assert encoder.d2h(d_out + f * ostride, int(lens[f])) == oracle.encode(frames[f], maxval, sub, *spec_tables), f
+    finally:
+        for p in (d_in, d_out, d_len):
+            encoder.free(p)
+
+
 def test_4k_quality90_444(encoder):
     """BASELINE config 2 workload at full size."""
     luma, chroma = dmmt_jpeg.quality_tables(90)
