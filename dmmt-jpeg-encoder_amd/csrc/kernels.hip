@@ -157,18 +157,21 @@ __device__ __forceinline__ void arai8(float (&v)[8]) {
 // round to the same integer, and as t is then no tie, rint (half to even) is
 // round half away from zero.  The other lanes (and NaN: maxval 0, q 0) redo d and
 // the division afterwards.
+// The eight distances are folded with max (three max3) before one compare; a
+// NaN (only from 0/0, maxval 0: `nan_possible`) would vanish in the max, so that
+// case always takes the exact path.
 __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const float* q, const float* crq,
-                                                     uint32_t (&out)[4]) {
+                                                     bool nan_possible, uint32_t (&out)[4]) {
     int x[8];
-    bool slow = false;
+    float dist = 0.0f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         const float t = u[r] * crq[8 * r];
         const float n = __builtin_rintf(t);
-        slow |= !(fabsf(t - n) < 0.4990234375f);  // 1/2 - 2^-10
+        dist = fmaxf(dist, fabsf(t - n));
         x[r] = (int)n;
     }
-    if (slow) {
+    if (nan_possible || !(dist < 0.4990234375f)) {  // 1/2 - 2^-10
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const float t = u[r] * crq[8 * r];
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                     quantize_col8(v, q, rq, qv[jj]);
                 } else {
                     arai8_unscaled(v);
-                    quantize_col8_scaled(v, q, rq, qv[jj]);
+                    quantize_col8_scaled(v, q, rq, g.maxval == 0, qv[jj]);
                 }
             }
         }
