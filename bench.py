@@ -33,6 +33,9 @@ import torch.distributed as dist  # noqa: E402
 import dmmt_jpeg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+# f32 VALU issue rate measured on MI355X by tools/pk_rate.hip: 64.2 T lane-ops/s of
+# independent v_add_f32 = 1.003 T wave64 instructions/s over the chip
+VALU_PEAK_PER_S = 1.003e12
 
 CONFIGS = {
     # name: (width, height, subsampling, quality, frames per step)
@@ -327,12 +330,23 @@ def main(argv=None, make_encoder=None, emit=None):
         path_bytes = algo_bytes + fps * jpeg_bytes
         path_achieved = path_bytes / (elapsed / args.steps) / 1e9
         traffic = None
+        valu = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get("front_hbm_bytes_per_launch")
+                pmc_d = json.load(open(pmc))
+                traffic = pmc_d.get("front_hbm_bytes_per_launch")
+                n_valu = pmc_d["kernels"]["k_front"].get("SQ_INSTS_VALU")
+                if n_valu:
+                    # the bound that does apply: VALU wave-instructions
+                    # per launch (PMC) / this launch time, against the issue rate
+                    # tools/pk_rate.hip measured (independent v_add_f32 streams)
+                    rate = n_valu / avg_front_s
+                    valu = {"wave_instructions_per_launch": round(n_valu), "achieved_per_s": round(rate, -6),
+                            "peak_per_s": VALU_PEAK_PER_S, "frac": round(rate / VALU_PEAK_PER_S, 4),
+                            "source": f"profiles/pmc_{args.config}.json SQ_INSTS_VALU; peak tools/pk_rate.hip"}
             except Exception:
-                traffic = None
+                traffic = valu = None
         ingest = ppm_ingest(enc, w, h, args.ppm_steps) if args.ppm_steps > 0 else None
         cpu = None
         if args.cpu_seconds > 0:
@@ -373,6 +387,7 @@ def main(argv=None, make_encoder=None, emit=None):
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "path": {"algorithmic_bytes_per_step": path_bytes, "achieved": round(path_achieved, 1),
                          "frac": round(path_achieved / HBM_PEAK_GBS, 4)},
+                "valu": valu,
             },
             "cpu_baseline": cpu,
             "ppm_ingest": ingest,
