@@ -349,7 +349,7 @@ def main(argv=None, make_encoder=None, emit=None):
                 traffic = valu = None
         ingest = ppm_ingest(enc, w, h, args.ppm_steps) if args.ppm_steps > 0 else None
         cpu = None
-        if args.cpu_seconds > 0:
+        if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
             from oracle.synth import synthetic  # numpy twin of the device generator
             rgb = synthetic(w, h, frame=0)
             cpu = cpu_baseline(rgb, sub, luma, chroma, args.cpu_seconds)
