@@ -564,8 +564,11 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
             }
             // r16 = 16 * (current zero run), so (run & 15) << 4 is r16 & 0xF0 and
             // run >> 4 is r16 >> 8; ZRLs are summed in a register, counted once
-            int r16 = 0;
-            if (half) {  // zeros after the last non-zero of positions 1..31
+            // l16 = 16 * (index of the last non-zero + 1), so the zero run before
+            // index kk is 16 * kk - l16 = 16 * run: (run & 15) << 4 is its & 0xF0
+            // and run >> 4 its >> 8; zero positions cost nothing here
+            int l16 = 16;  // half 0: the DC at index 0
+            if (half) {    // the zeros after the last non-zero of positions 1..31 carry over
                 const uint4* lo = reinterpret_cast<const uint4*>(sCoef + blk * CS);
                 uint32_t nzm = 0;  // bit k: position k non-zero
 #pragma unroll
@@ -580,7 +583,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                     }
                 }
                 nzm &= ~1u;  // not the DC
-                r16 = 16 * (nzm ? 31 - (31 - __clz((int)nzm)) : 31);
+                l16 = -16 * (nzm ? __clz((int)nzm) : 31);
             }
             uint32_t* h = sHist + ((blk % BPM) < NLUMA ? 0 : 256) + 513 * (blk % HC);
             uint32_t zrl = 0;
@@ -592,14 +595,15 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                     // Image<f32> dots only (integer samples bound |v| by 2049): -32768
                     // has no category (categorize.rs:25-30)
                     if (SB == 4 && v == -32768) bad |= 4;
-                    if (r16 >= 256) zrl += (uint32_t)(r16 >> 8);
+                    const int r16 = 16 * kk - l16;
+                    if (r16 >= 256) zrl += (uint32_t)(r16 >> 8);  // (rare: a branch, not two VALU ops)
                     atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
-                    r16 = -16;
+                    l16 = 16 * kk + 16;
                 }
-                r16 += 16;
             }
             if (zrl) atomicAdd(&h[0xF0], zrl);
             if (half) {
+                const int r16 = 16 * 32 - l16;  // trailing zeros
                 if (r16) atomicAdd(&h[0], 1u);                     // EOB
                 lastnz[e0 + blk] = (uint8_t)(63 - (r16 >> 4));  // k_emit groups its walks by this
             }
