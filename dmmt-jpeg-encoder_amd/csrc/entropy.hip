@@ -114,21 +114,23 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
         sink(((e & 0xFFFFu) << cat) | extra_bits(dcd, cat), (int)(e >> 16) + cat);
     }
     const uint32_t z = actab[0xF0];
-    int r16 = 0;  // 16 * (current zero run): (run & 15) << 4 is r16 & 0xF0
+    // l16 = 16 * (position of the last non-zero + 1): the zero run before position
+    // k is r16 / 16 with r16 = 16 * k - l16, (run & 15) << 4 = r16 & 0xF0
+    int l16 = 16;
 #pragma unroll
     for (int k = 1; k < 64; ++k) {
         if (k > kmax) continue;  // (wave-uniform) every later position is zero in every lane
         const int v = coef_at(b, k);
         if (v != 0) {
+            const int r16 = 16 * k - l16;
             for (int r = r16 >> 8; r > 0; --r) sink(z & 0xFFFFu, (int)(z >> 16));
             const int cat = category_fast(v);
             const uint32_t e = actab[(r16 & 0xF0) | cat];
             sink(((e & 0xFFFFu) << cat) | extra_bits(v, cat), (int)(e >> 16) + cat);
-            r16 = -16;
+            l16 = 16 * k + 16;
         }
-        r16 += 16;
     }
-    if (r16 || kmax < 63) {
+    if (l16 < 16 * 64 || kmax < 63) {
         const uint32_t e = actab[0];  // EOB
         sink(e & 0xFFFFu, (int)(e >> 16));
     }
@@ -194,7 +196,8 @@ struct SlotSink {
         nacc += len;
         if (nacc >= 32) {
             nacc -= 32;
-            if (wi < kSlotWords) slot[wi * 256] = (uint32_t)(acc >> nacc);
+            // past the slot the word lands in its last one: the chunk re-walks then
+            slot[min(wi, kSlotWords - 1) * 256] = (uint32_t)(acc >> nacc);
             ++wi;
         }
     }
