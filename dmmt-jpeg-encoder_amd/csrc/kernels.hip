@@ -312,9 +312,11 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     constexpr int CB = TM;           // chroma blocks per component
     constexpr int BS = 72;           // LDS floats per block: 64 + pad (conflict-free column reads)
     constexpr int CS = 72;           // int16 block stride of the quantised image (144 B: conflict-free 16-B reads)
-    constexpr int NJ = 8 * CB;       // fused jobs (chroma row, chroma block)
+    constexpr int SP = HR;           // threads per (chroma row, chroma block): one per luma block column
+    constexpr int NJ = 8 * CB * SP;  // fused jobs (chroma row, chroma block, luma block column): 256
+    constexpr int NCS = 8 / SP;      // chroma samples of a job
     constexpr int SB = (int)sizeof(Sample);
-    constexpr int PXB = 8 * HR * 3 * SB;  // raw bytes of one job row
+    constexpr int PXB = 8 * 3 * SB;  // raw bytes of one job row (8 pixels)
     constexpr int PXW = PXB / 4;
     constexpr int NCJ = NB * 8;      // column jobs
     constexpr int JPT = (NCJ + 255) / 256;
@@ -380,8 +382,9 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
         // not for u8 samples with maxval 255 or u16 with 65535 (the PPM norm)
         auto phase_a = [&](auto range_check) {
             constexpr bool CHECK = decltype(range_check)::value;
-            const int c = tid % CB, r = tid / CB;  // chroma block, chroma row
-            const int lx0 = c * 8 * HR;            // first pixel column of the job
+            const int h = tid % SP, job = tid / SP;
+            const int c = job % CB, r = job / CB;  // chroma block, chroma row
+            const int lx0 = c * 8 * HR + 8 * h;    // first pixel column of the job
             uint32_t pw[VR][SB == 4 ? 1 : PXW];    // raw bytes of the job's VR pixel rows (integer samples)
             const float* fsrc[VR];                 // the rows themselves (float samples)
 #pragma unroll
@@ -406,11 +409,11 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                                     ((uint32_t)src[4 * k + 2] << 16) | ((uint32_t)src[4 * k + 3] << 24);
                 }
             }
-            float yv[VR][HR][8];
-            float cbv[8], crv[8];
+            float yv[VR][8];
+            float cbv[8], crv[8];  // (4:2:x: the job's NCS = 4 samples first)
             uint32_t smax = 0;  // largest sample of the job (a sample above maxval panics in color.rs:63-65)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {  // chroma sample k of the row
+            for (int k = 0; k < NCS; ++k) {  // chroma sample k of the job
                 float cbs = 0.0f, crs = 0.0f;
 #pragma unroll
                 for (int dx = 0; dx < HR; ++dx) {
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                         }
                         float y, cb, cr;
                         rgb_to_ycbcr(rr, gg, bb, y, cb, cr);
-                        yv[dy][jx >> 3][jx & 7] = y;
+                        yv[dy][jx] = y;
                         if (dx == 0 && dy == 0) {
                             cbs = cb;
                             crs = cr;
@@ -464,22 +467,38 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
 #pragma unroll
             for (int dy = 0; dy < VR; ++dy) {
                 const int ly = r * VR + dy;
-#pragma unroll
-                for (int jb = 0; jb < HR; ++jb) {
-                    arai8(yv[dy][jb]);
-                    float4* o = reinterpret_cast<float4*>(sT + ((ly >> 3) * 32 + c * HR + jb) * BS + (ly & 7) * 8);
-                    o[0] = make_float4(yv[dy][jb][0], yv[dy][jb][1], yv[dy][jb][2], yv[dy][jb][3]);
-                    o[1] = make_float4(yv[dy][jb][4], yv[dy][jb][5], yv[dy][jb][6], yv[dy][jb][7]);
-                }
+                arai8(yv[dy]);
+                float4* o = reinterpret_cast<float4*>(sT + ((ly >> 3) * 32 + c * HR + h) * BS + (ly & 7) * 8);
+                o[0] = make_float4(yv[dy][0], yv[dy][1], yv[dy][2], yv[dy][3]);
+                o[1] = make_float4(yv[dy][4], yv[dy][5], yv[dy][6], yv[dy][7]);
             }
-            arai8(cbv);
-            arai8(crv);
-            float4* ob = reinterpret_cast<float4*>(sT + (NYB + c) * BS + r * 8);
-            ob[0] = make_float4(cbv[0], cbv[1], cbv[2], cbv[3]);
-            ob[1] = make_float4(cbv[4], cbv[5], cbv[6], cbv[7]);
-            float4* orr = reinterpret_cast<float4*>(sT + (NYB + CB + c) * BS + r * 8);
-            orr[0] = make_float4(crv[0], crv[1], crv[2], crv[3]);
-            orr[1] = make_float4(crv[4], crv[5], crv[6], crv[7]);
+            if constexpr (SP == 1) {
+                arai8(cbv);
+                arai8(crv);
+                float4* ob = reinterpret_cast<float4*>(sT + (NYB + c) * BS + r * 8);
+                ob[0] = make_float4(cbv[0], cbv[1], cbv[2], cbv[3]);
+                ob[1] = make_float4(cbv[4], cbv[5], cbv[6], cbv[7]);
+                float4* orr = reinterpret_cast<float4*>(sT + (NYB + CB + c) * BS + r * 8);
+                orr[0] = make_float4(crv[0], crv[1], crv[2], crv[3]);
+                orr[1] = make_float4(crv[4], crv[5], crv[6], crv[7]);
+            } else {
+                // the pair (h = 0, 1) holds chroma samples 0..3 and 4..7 of the row:
+                // h = 0 takes the row pass of Cb, h = 1 that of Cr, each swapping
+                // the four samples the other needs (DPP quad_perm [1,0,3,2]: lane ^ 1)
+                float fr[8];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float send = h ? cbv[k] : crv[k];
+                    const float recv = __int_as_float(
+                        __builtin_amdgcn_update_dpp(0, __float_as_int(send), 0xB1, 0xF, 0xF, false));
+                    fr[k] = h ? recv : cbv[k];
+                    fr[4 + k] = h ? crv[k] : recv;
+                }
+                arai8(fr);
+                float4* oc = reinterpret_cast<float4*>(sT + (NYB + (h ? CB : 0) + c) * BS + r * 8);
+                oc[0] = make_float4(fr[0], fr[1], fr[2], fr[3]);
+                oc[1] = make_float4(fr[4], fr[5], fr[6], fr[7]);
+            }
         };
         if (tid < NJ) {
             if (check_range)
