@@ -285,10 +285,12 @@ struct RawTile {
 // MCU row (256 padded pixel columns, 8*VR rows), looping over the frame's tiles
 // (grid = resident workgroups; blockIdx.y = frame) with the next tile's pixels
 // prefetched into registers while the current one computes.
-//  A  colour + subsampling + row DCT, fused: one thread per (chroma row, chroma
-//     block) converts its 8*HR x VR pixels (raw bytes from LDS), box-averages the
-//     chroma in the reference's sum order and runs the row pass of the HR*VR luma
-//     rows and the two chroma rows in registers -> block-major LDS (stride BS)
+//  A  colour + subsampling + row DCT, fused: one thread per (chroma row, luma
+//     block column) converts its 8 x VR pixels (raw bytes from LDS), box-averages
+//     the chroma in the reference's sum order and runs the row pass of its VR
+//     luma rows and of the chroma rows in registers -> block-major LDS (stride
+//     BS); with 4:2:x the two threads of a chroma block swap four chroma samples
+//     over DPP and take one chroma row pass each
 //  C  column DCT + quantise (quantize_col8_scaled): one lane per (block, column); results
 //     held in registers across a barrier, then scattered in zigzag order into the
 //     (aliased) int16 block image in local MCU emission order
