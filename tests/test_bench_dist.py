@@ -104,3 +104,27 @@ def test_bench_two_ranks_gloo(tmp_path):
     expect = w * h * fps * 20 * world / (line["ms_per_step"] * 20 / 1e3) / 1e6
     assert line["value"] == pytest.approx(expect, rel=2e-3)
     assert line["config"]["parallelism"] == "independent frames x2"
+
+
+def test_bench_line_fields_single_rank(monkeypatch):
+    """N = 1, the BASELINE config (4K 4:4:4 q90): the roofline block carries the
+    HBM view of k_front and, from the committed PMC counters, its VALU view."""
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    import bench
+    log, lines = [], []
+    bench.main(["--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0"],
+               make_encoder=lambda lr: StandInEncoder(lr, 0, log), emit=lines.append)
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["metric"] == "Mpixel/s encoded (4K PPM, q=90)"
+    rf = line["roofline"]
+    assert rf["kernel"] == "k_front" and rf["peak"] == 8000.0 and rf["unit"] == "GB/s"
+    assert rf["algorithmic_bytes_per_launch"] == 3840 * 2160 * 3
+    assert rf["avg_launch_us"] == pytest.approx(50.0)  # the stand-in's profile(): 0.15 ms over 3 launches
+    assert rf["frac"] == pytest.approx(rf["achieved"] / 8000.0, rel=1e-2)
+    pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_4k444q90.json")))
+    assert rf["traffic"] == pmc["front_hbm_bytes_per_launch"]
+    v = rf["valu"]
+    assert v["wave_instructions_per_launch"] == round(pmc["kernels"]["k_front"]["SQ_INSTS_VALU"])
+    assert v["frac"] == pytest.approx(v["wave_instructions_per_launch"] / 50e-6 / bench.VALU_PEAK_PER_S, rel=1e-3)
+    assert line["cpu_baseline"] is None and line["ppm_ingest"] is None
