@@ -291,3 +291,34 @@ def test_cli_and_convert_ppm(tmp_path, spec_tables):
     assert out2.read_bytes() == oracle.encode(rgb, mx, 2, *spec_tables)
     r = subprocess.run([dmmt_jpeg.CLI_PATH, str(tmp_path / "missing.ppm"), str(out)], capture_output=True)
     assert r.returncode == 1 and b"Conversion failed because of" in r.stderr
+
+
+def test_seeded_random_sweep(encoder):
+    """200 seeded random cases across the option space, each byte-compared with the
+    oracle: shape (1..300 x 1..300), subsampling, IJG quality 1..100, 8/16-bit
+    samples with any maxval, sample content (noise, smooth, flat, sparse), restart
+    interval (0 or 1..40 MCUs)."""
+    rng = np.random.default_rng(20261016)
+    for case in range(200):
+        h, w = int(rng.integers(1, 301)), int(rng.integers(1, 301))
+        sub = int(rng.integers(0, 3))
+        q = int(rng.integers(1, 101))
+        maxval = int(rng.choice([255, int(rng.integers(1, 256)), int(rng.integers(256, 65536))]))
+        kind = int(rng.integers(0, 4))
+        if kind == 0:
+            px = rng.integers(0, maxval + 1, (h, w, 3))
+        elif kind == 1:
+            yy, xx = np.mgrid[0:h, 0:w]
+            px = ((np.stack([xx, yy, xx + yy], -1) * maxval) // max(w + h, 1)) % (maxval + 1)
+        elif kind == 2:
+            px = np.full((h, w, 3), int(rng.integers(0, maxval + 1)))
+        else:
+            px = np.where(rng.random((h, w, 3)) < 0.02, rng.integers(0, maxval + 1, (h, w, 3)), 0)
+        rgb = px.astype(np.uint8 if maxval < 256 else np.uint16)
+        ri = 0 if rng.random() < 0.5 else int(rng.integers(1, 41))
+        luma, chroma = dmmt_jpeg.quality_tables(q)
+        o = opts(sub, luma, chroma)
+        o.restart_interval = ri
+        gpu = encoder.encode(dmmt_jpeg.Image.from_array(rgb, maxval), o)
+        ref = oracle.encode(rgb, maxval, sub, luma, chroma, restart_interval=ri)
+        assert gpu == ref, dict(case=case, h=h, w=w, sub=sub, q=q, maxval=maxval, kind=kind, ri=ri)
