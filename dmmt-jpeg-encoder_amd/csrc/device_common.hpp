@@ -70,6 +70,18 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
+// wave_sum_u32 over DPP, no LDS: quad sums (lane ^ 1, lane ^ 2), then mirrored
+// half rows and rows, then the four row sums read out.  All 64 lanes must be
+// active (a row sum is read from lanes 0, 16, 32, 48).
+__device__ __forceinline__ uint32_t wave_sum_full_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
     const int lane = lane_id();
 #pragma unroll

@@ -366,10 +366,15 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
         __syncthreads();
     }
     DMMT_TRACE(2);
+    // the eight residue counts two to a word (16-bit fields: a wave's count stays
+    // below 64 * 4 * 56 < 2^16), summed over the wave by DPP
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const uint32_t v = wave_sum_u32(ff[r]);
-        if (lane == 0 && v) atomicAdd(&sFF[r], v);
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t v = wave_sum_full_u32(ff[2 * r] | (ff[2 * r + 1] << 16));
+        if (lane == 0 && v) {
+            atomicAdd(&sFF[2 * r], v & 0xFFFFu);
+            atomicAdd(&sFF[2 * r + 1], v >> 16);
+        }
     }
     __syncthreads();
     if (tid < 8) chunk_ff[cid * 8 + tid] = sFF[tid];
