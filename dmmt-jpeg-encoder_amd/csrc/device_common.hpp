@@ -82,6 +82,22 @@ __device__ __forceinline__ uint32_t wave_sum_full_u32(uint32_t v) {
            (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+// wave_incl_scan_u32 over DPP, no LDS (the classic GCN row scan: shifts by 1, 2,
+// 3 of the inputs, 4 and 8 of the partial sums, then the row broadcasts 15 and
+// 31).  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan_full_u32(uint32_t v) {
+    const int s = (int)v;
+    int x = s;
+    x += __builtin_amdgcn_update_dpp(0, s, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, s, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, s, 0x113, 0xF, 0xF, true);  // row_shr:3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xE, true);  // row_shr:4, lanes 4-15 of a row
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xC, true);  // row_shr:8, lanes 8-15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false); // row_bcast:15 into rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false); // row_bcast:31 into rows 2, 3
+    return (uint32_t)x;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
     const int lane = lane_id();
 #pragma unroll

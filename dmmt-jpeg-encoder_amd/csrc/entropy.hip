@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     __syncthreads();
     if (tid < 64) {
         const uint32_t c = sBin[tid];
-        const uint32_t inc = wave_incl_scan_u32(c);
+        const uint32_t inc = wave_incl_scan_full_u32(c);  // (wave 0 whole)
         sBin[tid] = inc - c;  // first position of bin tid
     }
     __syncthreads();
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     // offsets inside the chunk by a workgroup scan; a block too long for its slot
     // sends the whole chunk down the re-walk path
     const bool over = __syncthreads_or(bits > (uint32_t)kSlotWords * 32u) != 0;
-    const uint32_t incl = wave_incl_scan_u32(bits);
+    const uint32_t incl = wave_incl_scan_full_u32(bits);
     if (lane == 63) sWave[wave] = incl;
     __syncthreads();
     uint32_t start = incl - bits;
