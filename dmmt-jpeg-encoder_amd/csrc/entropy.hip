@@ -704,7 +704,7 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
                 cnt += (uint32_t)__popc(~nonzero & vmask);
             }
         }
-        const uint32_t incl = wave_incl_scan_u32(cnt);
+        const uint32_t incl = wave_incl_scan_full_u32(cnt);
         if (lane == 63) sWave[wave] = incl;
         __syncthreads();
         uint32_t pre = incl - cnt;

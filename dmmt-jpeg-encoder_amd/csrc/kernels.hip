@@ -912,7 +912,7 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
     {
         const int rk = n - 1 - s;  // rank at reversed position s
         const uint32_t wgt = sym_thread && s < n ? 1u << (16 - sLen[rk]) : 0u;
-        const uint32_t incl = wave_incl_scan_u32(wgt);
+        const uint32_t incl = wave_incl_scan_full_u32(wgt);
         if (sym_thread && lane == 63) sWave[wave] = incl;
         __syncthreads();
         uint32_t excl = incl - wgt;
