@@ -108,6 +108,27 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
     return v;
 }
 
+// wave_incl_scan_u64 over DPP (the pattern of wave_incl_scan_full_u32 on both
+// halves, added as 64-bit).  All 64 lanes must be active.
+template <int CTRL, int ROW_MASK, int BANK_MASK, bool BOUND_CTRL>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp(0, lo, CTRL, ROW_MASK, BANK_MASK, BOUND_CTRL);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp(0, hi, CTRL, ROW_MASK, BANK_MASK, BOUND_CTRL);
+    return ((unsigned long long)h << 32) | l;
+}
+__device__ __forceinline__ unsigned long long wave_incl_scan_full_u64(unsigned long long v) {
+    unsigned long long x = v;
+    x += dpp_u64<0x111, 0xF, 0xF, true>(v);
+    x += dpp_u64<0x112, 0xF, 0xF, true>(v);
+    x += dpp_u64<0x113, 0xF, 0xF, true>(v);
+    x += dpp_u64<0x114, 0xF, 0xE, true>(x);
+    x += dpp_u64<0x118, 0xF, 0xC, true>(x);
+    x += dpp_u64<0x142, 0xA, 0xF, false>(x);
+    x += dpp_u64<0x143, 0xC, 0xF, false>(x);
+    return x;
+}
+
 __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long v) {
     const int lane = lane_id();
 #pragma unroll

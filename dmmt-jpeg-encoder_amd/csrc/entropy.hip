@@ -437,7 +437,7 @@ __device__ __forceinline__ unsigned long long chunk_out_bytes(const uint32_t* __
 __device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long v, unsigned long long* sWave,
                                                               unsigned long long* tot) {
     const int lane = lane_id(), wave = threadIdx.x >> 6;
-    const unsigned long long incl = wave_incl_scan_u64(v);
+    const unsigned long long incl = wave_incl_scan_full_u64(v);  // (all 1024 threads take part)
     if (lane == 63) sWave[wave] = incl;
     __syncthreads();
     unsigned long long pre = incl - v, all = 0;

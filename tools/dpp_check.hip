@@ -5,7 +5,10 @@ __global__ void k(const unsigned* in, unsigned* a, unsigned* b, unsigned* c) {
     unsigned v = in[blockIdx.x * 256 + threadIdx.x];
     a[blockIdx.x * 256 + threadIdx.x] = dmmt::wave_incl_scan_full_u32(v);
     b[blockIdx.x * 256 + threadIdx.x] = dmmt::wave_incl_scan_u32(v);
-    c[blockIdx.x * 256 + threadIdx.x] = dmmt::wave_sum_full_u32(v) - dmmt::wave_sum_u32(v);
+    // 64-bit: values across the 2^32 carry
+    const unsigned long long w = ((unsigned long long)v << 20) * 3ull + 0xFFFFF000ull;
+    c[blockIdx.x * 256 + threadIdx.x] = (dmmt::wave_sum_full_u32(v) - dmmt::wave_sum_u32(v)) +
+                                        (dmmt::wave_incl_scan_full_u64(w) != dmmt::wave_incl_scan_u64(w) ? 1u : 0u);
 }
 int main() {
     const int N = 256 * 64;
