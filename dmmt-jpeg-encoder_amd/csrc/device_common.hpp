@@ -82,6 +82,15 @@ __device__ __forceinline__ uint32_t wave_sum_full_u32(uint32_t v) {
            (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+// The previous / next lane's value across the whole wave (DPP wave_shr:1 /
+// wave_shl:1; 0 in lane 0 / lane 63).  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t lane_prev_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t lane_next_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+
 // wave_incl_scan_u32 over DPP, no LDS (the classic GCN row scan: shifts by 1, 2,
 // 3 of the inputs, 4 and 8 of the partial sums, then the row broadcasts 15 and
 // 31).  All 64 lanes must be active.

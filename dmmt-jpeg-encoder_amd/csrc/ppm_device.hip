@@ -290,7 +290,7 @@ __device__ __forceinline__ void fast_window(const PpmText& t, long long pos, Fas
 // the previous thread's last (a shuffle) or, for lane 0, read back
 __device__ __forceinline__ unsigned long long fast_starts(const FastWin& W) {
     const unsigned long long sig = W.valid & ~W.ws;
-    uint32_t prev = (uint32_t)__shfl_up((int)(uint32_t)(sig >> 63), 1, 64);
+    uint32_t prev = lane_prev_u32((uint32_t)(sig >> 63));  // (the wave is whole here)
     if (lane_id() == 0) prev = W.prev_sig;
     return sig & ~((sig << 1) | prev);
 }
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* 
     const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
     FastWin F;
     fast_window(t, pos, F, false);
-    const uint32_t n = wave_sum_u32((uint32_t)__popcll(fast_starts(F)));
+    const uint32_t n = wave_sum_full_u32((uint32_t)__popcll(fast_starts(F)));
     if (lane_id() == 0) sRed[tid >> 6] = n;
     const bool hash = __syncthreads_or(F.hash) != 0;
     if (tid == 0) {
@@ -423,16 +423,16 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
     const unsigned long long starts = fast_starts(F);
     const uint32_t n = (uint32_t)__popcll(starts);
     const unsigned long long ends = F.ws | ~F.valid;  // bytes that end a token
-    uint32_t wn = (uint32_t)__shfl_down((int)F.w[0], 1, 64);
-    uint32_t next4 = (uint32_t)__shfl_down((int)(uint32_t)(ends & 0xFull), 1, 64) & 0xFu;
+    uint32_t wn = lane_next_u32(F.w[0]);
+    uint32_t next4 = lane_next_u32((uint32_t)(ends & 0xFull)) & 0xFu;
     if (lane == 63) {  // the next window belongs to the next wave (or chunk)
         wn = F.next_w;
         next4 = F.next_end;
     }
-    const uint32_t inc = wave_incl_scan_u32(n);
+    const uint32_t inc = wave_incl_scan_full_u32(n);
     if (lane == 63) sWave[wave] = inc;
     if (wave == 0) {
-        cnt = wave_sum_u32(cnt);
+        cnt = wave_sum_full_u32(cnt);
         if (lane == 0) sBase = row_base[blockIdx.x / per] + cnt;
     }
     __syncthreads();
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(kPpmCarryThreads) void k_ppm_carry(const uint32_t* 
                 if (kb + 4 * u + 4 >= r0 + rper) break;
             }
         }
-        const unsigned long long inc = wave_incl_scan_u64(s);
+        const unsigned long long inc = wave_incl_scan_full_u64(s);
         if (lane_id() == 63) sSum[t >> 6] = inc;
         __syncthreads();
         unsigned long long base = inc - s;

@@ -7,8 +7,12 @@ __global__ void k(const unsigned* in, unsigned* a, unsigned* b, unsigned* c) {
     b[blockIdx.x * 256 + threadIdx.x] = dmmt::wave_incl_scan_u32(v);
     // 64-bit: values across the 2^32 carry
     const unsigned long long w = ((unsigned long long)v << 20) * 3ull + 0xFFFFF000ull;
+    const unsigned prev = (unsigned)__shfl_up((int)v, 1, 64), next = (unsigned)__shfl_down((int)v, 1, 64);
+    const int lane = threadIdx.x & 63;
     c[blockIdx.x * 256 + threadIdx.x] = (dmmt::wave_sum_full_u32(v) - dmmt::wave_sum_u32(v)) +
-                                        (dmmt::wave_incl_scan_full_u64(w) != dmmt::wave_incl_scan_u64(w) ? 1u : 0u);
+                                        (dmmt::wave_incl_scan_full_u64(w) != dmmt::wave_incl_scan_u64(w) ? 1u : 0u) +
+                                        (dmmt::lane_prev_u32(v) != (lane ? prev : 0u) ? 1u : 0u) +
+                                        (dmmt::lane_next_u32(v) != (lane < 63 ? next : 0u) ? 1u : 0u);
 }
 int main() {
     const int N = 256 * 64;
