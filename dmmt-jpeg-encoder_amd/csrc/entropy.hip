@@ -463,29 +463,28 @@ __device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigne
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     bool fi = f;
     unsigned long long vi = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {  // inclusive within the wave
-        const unsigned long long pv = __shfl_up(vi, d, 64);
-        const int pf = __shfl_up((int)fi, d, 64);
-        if (lane >= d) {
-            bool ff = pf != 0;
-            unsigned long long vv = pv;
-            seg_combine(ff, vv, fi, vi);
-            fi = ff;
-            vi = vv;
-        }
-    }
+    // inclusive within the wave over DPP: row shifts 1, 2, 4, 8 (a lane without a
+    // source gets (0, false), the identity), then the row broadcasts 15 and 31;
+    // the earlier element is always the left operand
+    auto step = [&](unsigned long long pv, int pf) {
+        bool ff = pf != 0;
+        seg_combine(ff, pv, fi, vi);
+        fi = ff;
+        vi = pv;
+    };
+    step(dpp_u64<0x111, 0xF, 0xF, true>(vi), __builtin_amdgcn_update_dpp(0, (int)fi, 0x111, 0xF, 0xF, true));
+    step(dpp_u64<0x112, 0xF, 0xF, true>(vi), __builtin_amdgcn_update_dpp(0, (int)fi, 0x112, 0xF, 0xF, true));
+    step(dpp_u64<0x114, 0xF, 0xF, true>(vi), __builtin_amdgcn_update_dpp(0, (int)fi, 0x114, 0xF, 0xF, true));
+    step(dpp_u64<0x118, 0xF, 0xF, true>(vi), __builtin_amdgcn_update_dpp(0, (int)fi, 0x118, 0xF, 0xF, true));
+    step(dpp_u64<0x142, 0xA, 0xF, false>(vi), __builtin_amdgcn_update_dpp(0, (int)fi, 0x142, 0xA, 0xF, false));
+    step(dpp_u64<0x143, 0xC, 0xF, false>(vi), __builtin_amdgcn_update_dpp(0, (int)fi, 0x143, 0xC, 0xF, false));
     if (lane == 63) {
         sWaveV[wave] = vi;
         sWaveF[wave] = fi;
     }
-    // exclusive within the wave
-    unsigned long long ve = __shfl_up(vi, 1, 64);
-    int fe = __shfl_up((int)fi, 1, 64);
-    if (lane == 0) {
-        ve = 0;
-        fe = 0;
-    }
+    // exclusive within the wave: the previous lane's inclusive value (lane 0: identity)
+    const unsigned long long ve = dpp_u64<0x138, 0xF, 0xF, true>(vi);
+    const int fe = __builtin_amdgcn_update_dpp(0, (int)fi, 0x138, 0xF, 0xF, true);
     __syncthreads();
     bool cf = false;
     unsigned long long cv = 0;
