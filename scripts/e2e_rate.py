@@ -20,8 +20,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="4k444q90", choices=sorted(bench.CONFIGS))
     ap.add_argument("--seconds", type=float, default=5.0)
+    ap.add_argument("--batch", type=int, default=0, help="frames per call (default: the config's)")
     a = ap.parse_args()
     w, h, sub, q, fps = bench.CONFIGS[a.config]
+    fps = a.batch or fps
     luma, chroma = dmmt_jpeg.quality_tables(q)
     opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
                                                chroma_table=chroma)
@@ -35,6 +37,7 @@ def main():
         n += 1
     dt = time.perf_counter() - t0
     print(json.dumps({"config": a.config, "mode": "host RGB -> host JPEG (PCIe both ways, dmmt_jpeg_encode_batch)",
+                      "frames_per_call": fps, "distinct_frames": min(fps, 8),
                       "mpixel_per_s": round(n * fps * w * h / dt / 1e6, 1), "calls": n,
                       "ms_per_call": round(dt / n * 1e3, 3), "mean_jpeg_bytes": sum(map(len, outs)) / len(outs)}))
     enc.close()

@@ -185,6 +185,19 @@ def test_batch_api_mixed_geometry(encoder, spec_tables):
         assert o == oracle.encode(a, 255, 2, *spec_tables)
 
 
+def test_batch_error_mid_batch(encoder, spec_tables):
+    """A sample above maxval in frame 2 of 4: the whole call fails (color.rs:63-65),
+    no output is returned, and the context stays usable."""
+    frames = [np.full((16, 24, 3), 90, np.uint8) for _ in range(4)]
+    frames[2][3, 5, 1] = 200
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        encoder.encode_batch([dmmt_jpeg.Image(24, 16, 100, f) for f in frames], opts(2, *spec_tables))
+    assert e.value.code == -100
+    ok = [synthetic(24, 16, frame=f) for f in range(3)]
+    outs = encoder.encode_batch([dmmt_jpeg.Image.from_array(a) for a in ok], opts(2, *spec_tables))
+    assert outs == [oracle.encode(a, 255, 2, *spec_tables) for a in ok]
+
+
 def test_device_resident_api_and_generator(encoder, spec_tables):
     w, h, n = 320, 240, 6
     d_in = encoder.malloc(w * h * 3 * n)
