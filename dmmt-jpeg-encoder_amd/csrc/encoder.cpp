@@ -51,8 +51,15 @@ constexpr size_t kMaxGraphs = 16;
 // One pipeline lane: a device workspace (grown on demand, never shrunk) and the
 // stream that runs on it.  Lane 0 is the context's own stream; dmmt_ctx_set_lanes
 // adds lanes so that consecutive dmmt_encode_device calls overlap.
+// Each lane has its own status words (sticky error bits the kernels OR in):
+// word kStatusAsync collects the asynchronous dmmt_encode_device calls run on the
+// lane and is reported by dmmt_ctx_synchronize; word kStatusSync belongs to the
+// synchronous host calls, which read and clear it before they return.  A host call
+// therefore never reports (or clears) an error of an earlier asynchronous encode.
+constexpr int kStatusAsync = 0, kStatusSync = 1;
 struct Lane {
     hipStream_t stream = nullptr;
+    DevBuf status;
     DevBuf coef, dc, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
         chunk_edge, chunk_bit0, chunk_out;
 };
@@ -64,8 +71,12 @@ struct dmmt_ctx {
     std::vector<Lane*> lanes;  // lanes[0].stream == stream
     int nlanes = 1;
     unsigned next_lane = 0;
-    // shared by the lanes: status word (sticky error bits) and the uploaded tables
-    DevBuf status, lut, qtab, qtab_u8;
+    // shared by the lanes: the uploaded tables
+    DevBuf lut, qtab, qtab_u8;
+    // asynchronous error bits already collected from lanes that were dropped
+    int async_bits = 0;
+    // orders calls on a caller's stream against lane 0 (whose workspace they use)
+    hipEvent_t ev_lane0 = nullptr, ev_caller = nullptr;
     // host-API staging
     DevBuf in, out, out_len, dct;
     // PPM ingest: file bytes, chunk maps / entry states, status + token count
@@ -194,7 +205,7 @@ int upload_tables(dmmt_ctx* c, const dmmt_options* opt, int maxval, int sb, hipS
     return DMMT_OK;
 }
 
-int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane) {
+int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool async) {
     int rc;
     Lane* L = c->lanes[lane];
     const size_t nb = (size_t)g.bpf * nf;
@@ -218,7 +229,7 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane) {
     if ((rc = ensure(L->code_tab, (size_t)nf * 1024 * 4))) return rc;
     if ((rc = ensure(L->hdr_len, (size_t)nf * 4))) return rc;
     if ((rc = ensure(L->total_out, (size_t)nf * 8))) return rc;
-    if ((rc = ensure(c->status, 16, true))) return rc;
+    if ((rc = ensure(L->status, 16, true))) return rc;
     w->coef = (int16_t*)L->coef.p;
     w->dc = (int16_t*)L->dc.p;
     w->dcdiff = (int16_t*)L->dcdiff.p;
@@ -234,7 +245,7 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane) {
     w->chunk_bit0 = (unsigned long long*)L->chunk_bit0.p;
     w->chunk_out = (unsigned long long*)L->chunk_out.p;
     w->total_out = (unsigned long long*)L->total_out.p;
-    w->status = (int*)c->status.p;
+    w->status = (int*)L->status.p + (async ? kStatusAsync : kStatusSync);
     w->norm_lut = nullptr;  // bound by prepare() after upload_tables
     w->qtab = nullptr;
     w->qtab_u8 = nullptr;
@@ -243,9 +254,9 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane) {
 
 // workspace + tables for one launch batch; every table pointer is valid on return
 int prepare(dmmt_ctx* c, const Geom& g, int nf, const dmmt_options* opt, int sb, hipStream_t st, Work* w,
-            int lane = 0) {
+            int lane = 0, bool async = false) {
     int rc;
-    if ((rc = ensure_work(c, g, nf, w, lane))) return rc;
+    if ((rc = ensure_work(c, g, nf, w, lane, async))) return rc;
     if ((rc = upload_tables(c, opt, g.maxval, sb, st))) return rc;
     w->norm_lut = (const float*)c->lut.p;
     w->qtab = (const float*)c->qtab.p;
@@ -348,10 +359,10 @@ void destroy_graphs(dmmt_ctx* c) {
 // Stage profiling needs per-kernel events, so it always launches directly.
 int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, int nf, const Geom& g,
                    const dmmt_options* opt, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st,
-                   int lane = 0) {
+                   int lane = 0, bool async = false) {
     Work w;
     int rc;
-    if ((rc = prepare(c, g, nf, opt, sb, st, &w, lane))) return rc;
+    if ((rc = prepare(c, g, nf, opt, sb, st, &w, lane, async))) return rc;
     const int bits = opt->bits_per_channel;
     if (!c->use_graphs || c->profile)
         return enqueue_direct(c, d_rgb, frame_stride, sb, nf, g, w, bits, out, out_stride, out_len, st);
@@ -395,18 +406,10 @@ int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, 
     return DMMT_OK;
 }
 
-// read and clear the device status word
-int take_status(dmmt_ctx* c, hipStream_t st) {
-    if (!c->status.p) return DMMT_OK;
-    int s = 0;
-    HIP_TRY(hipMemcpyAsync(&s, c->status.p, sizeof s, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (s) {
-        HIP_TRY(hipMemsetAsync(c->status.p, 0, sizeof(int), st));
-        HIP_TRY(hipStreamSynchronize(st));
-    }
-    // in the reference's order: the sample range is checked when the PPM is read,
-    // categories while the blocks are categorised, symbols while they are written
+// error bits -> error code, in the reference's order: the sample range is checked
+// when the PPM is read, categories while the blocks are categorised, symbols while
+// they are written
+int status_code(int s) {
     if (s & 1) return DMMT_E_VALUE_EXCEEDS_MAX;
     if (s & 4) return DMMT_E_CATEGORY_RANGE;
     if (s & 2) return DMMT_E_HUFFMAN_SYMBOL_MISSING;
@@ -414,11 +417,40 @@ int take_status(dmmt_ctx* c, hipStream_t st) {
     return DMMT_OK;
 }
 
+// read and clear one status word of a lane (after the work on `st` that writes it)
+int read_status(Lane* L, int word, hipStream_t st, int* bits) {
+    *bits = 0;
+    if (!L->status.p) return DMMT_OK;
+    int* p = (int*)L->status.p + word;
+    HIP_TRY(hipMemcpyAsync(bits, p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (*bits) {
+        HIP_TRY(hipMemsetAsync(p, 0, sizeof(int), st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return DMMT_OK;
+}
+
+// the error of the synchronous host call that just ran on lane 0 (stream st)
+int take_status(dmmt_ctx* c, hipStream_t st) {
+    int s = 0, rc;
+    if ((rc = read_status(c->lanes[0], kStatusSync, st, &s))) return rc;
+    return status_code(s);
+}
+
+// fold the asynchronous error bits of a lane (idle: after sync_lanes) into async_bits
+int collect_async(dmmt_ctx* c, Lane* L) {
+    int s = 0, rc;
+    if ((rc = read_status(L, kStatusAsync, L->stream, &s))) return rc;
+    c->async_bits |= s;
+    return DMMT_OK;
+}
+
 int set_device(dmmt_ctx* c) { return hip_err(hipSetDevice(c->device)); }
 
 void destroy_lane(Lane* L, bool own_stream) {
     (void)hipStreamSynchronize(L->stream);
-    DevBuf* bufs[] = {&L->coef,     &L->dc,        &L->dcdiff,     &L->lastnz,     &L->ac_hist,
+    DevBuf* bufs[] = {&L->status,   &L->coef,      &L->dc,         &L->dcdiff,     &L->lastnz,     &L->ac_hist,
                       &L->dc_hist,  &L->code_tab,  &L->hdr_len,    &L->total_out,  &L->stage,
                       &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out};
     for (DevBuf* b : bufs) release(*b);
@@ -456,6 +488,11 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
     }
     c->lanes.push_back(new Lane());
     c->lanes[0]->stream = c->stream;
+    if (hipEventCreateWithFlags(&c->ev_lane0, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming) != hipSuccess) {
+        dmmt_ctx_destroy(c);
+        return DMMT_E_HIP;
+    }
     *out = c;
     return DMMT_OK;
 }
@@ -468,7 +505,9 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     destroy_graphs(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
     for (size_t i = 0; i < c->lanes.size(); ++i) destroy_lane(c->lanes[i], i > 0);
-    DevBuf* bufs[] = {&c->status, &c->lut, &c->qtab, &c->qtab_u8, &c->in, &c->out, &c->out_len, &c->dct};
+    if (c->ev_lane0) (void)hipEventDestroy(c->ev_lane0);
+    if (c->ev_caller) (void)hipEventDestroy(c->ev_caller);
+    DevBuf* bufs[] = {&c->lut, &c->qtab, &c->qtab_u8, &c->in, &c->out, &c->out_len, &c->dct};
     for (DevBuf* b : bufs) release(*b);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -480,7 +519,8 @@ extern "C" int dmmt_ctx_set_lanes(dmmt_ctx* c, int n) {
     int rc;
     if ((rc = set_device(c))) return rc;
     if ((rc = sync_lanes(c))) return rc;
-    while ((int)c->lanes.size() > n) {  // the workspaces of dropped lanes are freed
+    while ((int)c->lanes.size() > n) {  // the workspaces of dropped lanes are freed (their errors kept)
+        if ((rc = collect_async(c, c->lanes.back()))) return rc;
         destroy_lane(c->lanes.back(), true);
         c->lanes.pop_back();
     }
@@ -504,7 +544,11 @@ extern "C" int dmmt_ctx_synchronize(dmmt_ctx* c) {
     int rc;
     if ((rc = set_device(c))) return rc;
     HIP_TRY(hipDeviceSynchronize());
-    return take_status(c, c->stream);
+    for (Lane* L : c->lanes)
+        if ((rc = collect_async(c, L))) return rc;
+    const int s = c->async_bits;
+    c->async_bits = 0;
+    return status_code(s);
 }
 
 extern "C" size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t subsampling) {
@@ -524,14 +568,22 @@ extern "C" int dmmt_encode_device(dmmt_ctx* c, const dmmt_device_frames* f, cons
     if (f->out_stride < max_jpeg_bytes(g)) return DMMT_E_CAPACITY;
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    int lane = 0;
-    if (!stream && c->nlanes > 1) {  // pipelined: the next lane's workspace and stream
-        lane = (int)(c->next_lane++ % (unsigned)c->nlanes);
-        st = c->lanes[lane]->stream;
+    if (stream) {
+        // the caller's stream runs on lane 0's workspace: it waits for the work
+        // already queued on lane 0, and lane 0 for this call, in both directions
+        hipStream_t st = (hipStream_t)stream;
+        HIP_TRY(hipEventRecord(c->ev_lane0, c->stream));
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_lane0, 0));
+        rc = enqueue_encode(c, f->d_rgb, f->frame_stride, f->sample_bytes, f->n_frames, g, opt, f->d_out,
+                            f->out_stride, f->d_out_len, st, 0, true);
+        HIP_TRY(hipEventRecord(c->ev_caller, st));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_caller, 0));
+        return rc;
     }
+    int lane = 0;  // pipelined: the next lane's workspace and stream
+    if (c->nlanes > 1) lane = (int)(c->next_lane++ % (unsigned)c->nlanes);
     return enqueue_encode(c, f->d_rgb, f->frame_stride, f->sample_bytes, f->n_frames, g, opt, f->d_out, f->out_stride,
-                          f->d_out_len, st, lane);
+                          f->d_out_len, c->lanes[lane]->stream, lane, true);
 }
 
 // Host-memory batch of equal-geometry images -> host JPEGs.
@@ -561,8 +613,8 @@ static int encode_host_group(dmmt_ctx* c, const dmmt_image* imgs, int n, const d
         if (L[i] == 0 || L[i] > out_stride) return DMMT_E_CAPACITY;
         uint8_t* h = (uint8_t*)malloc(L[i]);
         if (!h) return DMMT_E_OUT_OF_MEMORY;
+        outs[i] = h;  // owned by the caller's cleanup from here on, even if the copy fails
         HIP_TRY(hipMemcpyAsync(h, (uint8_t*)c->out.p + out_stride * i, L[i], hipMemcpyDeviceToHost, st));
-        outs[i] = h;
         lens[i] = L[i];
     }
     HIP_TRY(hipStreamSynchronize(st));

@@ -118,6 +118,10 @@ typedef struct dmmt_ctx dmmt_ctx;
 int dmmt_ctx_create(int device, dmmt_ctx** out);
 void dmmt_ctx_destroy(dmmt_ctx* ctx);
 int dmmt_device_count(int* count);
+/* Waits for all work of the context (every lane, and caller streams the context's
+ * device runs) and returns the first error of the asynchronous dmmt_encode_device
+ * calls made since the last synchronize (then clears it).  The synchronous calls
+ * report their own errors and never those of asynchronous ones. */
 int dmmt_ctx_synchronize(dmmt_ctx* ctx);
 
 /* ---- the encoder seam --------------------------------------------------------------- */
@@ -131,7 +135,8 @@ int dmmt_jpeg_encode(dmmt_ctx* ctx, const dmmt_image* img, const dmmt_options* o
 int dmmt_jpeg_encode_batch(dmmt_ctx* ctx, const dmmt_image* imgs, int n, const dmmt_options* opt,
                            uint8_t** outs, size_t* lens);
 /* Device-resident form: frames in HBM -> JPEG files in HBM, enqueued on `stream`
- * (a hipStream_t, NULL = the context's stream), no host synchronisation. */
+ * (a hipStream_t, NULL = the context's stream), no host synchronisation.  Errors the
+ * kernels find (a sample above maxval, ...) are reported by dmmt_ctx_synchronize. */
 int dmmt_encode_device(dmmt_ctx* ctx, const dmmt_device_frames* frames, const dmmt_options* opt, void* stream);
 /* Pipelined device encodes (extension of the above; the reference encodes one image at a
  * time on the host): with n lanes (1..DMMT_MAX_LANES, default 1) a context keeps n
@@ -139,7 +144,9 @@ int dmmt_encode_device(dmmt_ctx* ctx, const dmmt_device_frames* frames, const dm
  * round-robin to them, so one call's latency-bound kernels (Huffman tables, offsets)
  * overlap the next calls' kernels.  Calls with stream NULL then run concurrently: their
  * inputs must be complete when the call is made, their outputs are complete after
- * dmmt_ctx_synchronize.  A non-NULL stream always uses lane 0, in stream order. */
+ * dmmt_ctx_synchronize.  A non-NULL stream always uses lane 0's workspace: the call waits
+ * (on the device) for the work already queued on lane 0, and later lane-0 work waits
+ * for it. */
 #define DMMT_MAX_LANES 8
 int dmmt_ctx_set_lanes(dmmt_ctx* ctx, int n);
 size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t subsampling);

@@ -1,4 +1,6 @@
-# parity suite, then the PCIe-inclusive host-batch rate with the frame pipeline off / on
+# parity suite, then the PCIe-inclusive host-batch rate (dmmt_jpeg_encode_batch) of the
+# current library for each config; the loop over variants keeps only 'default' since
+# the frame pipeline was reverted (A/B runs build the variant libraries themselves)
 set -o pipefail
 mkdir -p gpurun_out/e2e
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/e2e/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/e2e/gpu_tests.log; exit 1; }

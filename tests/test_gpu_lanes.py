@@ -77,3 +77,88 @@ def test_set_lanes_bounds(encoder):
             encoder.set_lanes(bad)
     encoder.set_lanes(8)
     encoder.set_lanes(1)
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_async_error_surfaces_at_synchronize(encoder, lanes):
+    """an asynchronous encode's error is reported by synchronize, never by (or lost
+    to) a host call made in between, whichever lane the bad frame ran on"""
+    w, h, sub = 64, 48, 0
+    opts = _opts(sub, 75)
+    good = synthetic(w, h, frame=3)
+    stride = dmmt_jpeg.max_jpeg_bytes(w, h, sub)
+    d_in = [encoder.malloc(good.nbytes) for _ in range(2)]
+    d_out = [encoder.malloc(stride) for _ in range(2)]
+    d_len = [encoder.malloc(4) for _ in range(2)]
+    try:
+        for d in d_in:
+            encoder.h2d(d, good)
+        encoder.set_lanes(lanes)
+        encoder.encode_device(d_in[0], 1, w, h, opts, d_out[0], stride, d_len[0])
+        # maxval 100 with samples up to 255: the RangeColorFormat panic (color.rs:63-65),
+        # on lane 1 with two lanes, on lane 0 with one
+        encoder.encode_device(d_in[1], 1, w, h, opts, d_out[1], stride, d_len[1], maxval=100)
+        assert encoder.encode(dmmt_jpeg.Image.from_array(good), opts) == \
+            oracle.encode(good, 255, sub, opts.luma_table, opts.chroma_table)
+        with pytest.raises(dmmt_jpeg.Error) as ei:
+            encoder.synchronize()
+        assert ei.value.name == "ValueExceedsMax"
+        encoder.synchronize()  # reported once, then clear
+        n = int(np.frombuffer(encoder.d2h(d_len[0], 4), np.uint32)[0])
+        assert encoder.d2h(d_out[0], n) == oracle.encode(good, 255, sub, opts.luma_table, opts.chroma_table)
+    finally:
+        encoder.set_lanes(1)
+        for d in d_in + d_out + d_len:
+            encoder.free(d)
+
+
+def test_async_error_kept_when_lanes_dropped(encoder):
+    w, h, sub = 40, 24, 1
+    opts = _opts(sub, 60)
+    bad = synthetic(w, h, frame=5)
+    stride = dmmt_jpeg.max_jpeg_bytes(w, h, sub)
+    d_in, d_out, d_len = encoder.malloc(bad.nbytes), encoder.malloc(stride), encoder.malloc(4)
+    try:
+        encoder.h2d(d_in, bad)
+        encoder.set_lanes(3)
+        encoder.encode_device(d_in, 1, w, h, opts, d_out, stride, d_len)  # lane 0
+        encoder.encode_device(d_in, 1, w, h, opts, d_out, stride, d_len)  # lane 1
+        encoder.encode_device(d_in, 1, w, h, opts, d_out, stride, d_len, maxval=7)  # lane 2: error
+        encoder.set_lanes(1)  # lane 2 is freed; its error is not
+        with pytest.raises(dmmt_jpeg.Error) as ei:
+            encoder.synchronize()
+        assert ei.value.name == "ValueExceedsMax"
+    finally:
+        encoder.set_lanes(1)
+        for d in (d_in, d_out, d_len):
+            encoder.free(d)
+
+
+def test_caller_stream_mixed_with_lanes(encoder):
+    """calls on a caller's stream use lane 0's workspace; interleaved with the
+    round-robin calls (lane 0 among them) every output stays exact"""
+    import torch
+    w, h, sub = 200, 136, 2
+    opts = _opts(sub, 85)
+    frames = [synthetic(w, h, frame=90 + i) for i in range(8)]
+    stride = dmmt_jpeg.max_jpeg_bytes(w, h, sub)
+    d_in = [encoder.malloc(f.nbytes) for f in frames]
+    d_out = [encoder.malloc(stride) for _ in frames]
+    d_len = [encoder.malloc(4) for _ in frames]
+    s = torch.cuda.Stream(device=0)
+    try:
+        for d, f in zip(d_in, frames):
+            encoder.h2d(d, f)
+        encoder.set_lanes(2)
+        for i in range(len(frames)):
+            stream = s.cuda_stream if i % 2 else None
+            encoder.encode_device(d_in[i], 1, w, h, opts, d_out[i], stride, d_len[i], stream=stream)
+        encoder.synchronize()
+        s.synchronize()
+        for i, f in enumerate(frames):
+            n = int(np.frombuffer(encoder.d2h(d_len[i], 4), np.uint32)[0])
+            assert encoder.d2h(d_out[i], n) == oracle.encode(f, 255, sub, opts.luma_table, opts.chroma_table), i
+    finally:
+        encoder.set_lanes(1)
+        for d in d_in + d_out + d_len:
+            encoder.free(d)
