@@ -1,0 +1,36 @@
+"""Encode one synthetic image several times (whole path and back half from the
+oracle's coefficients) and report whether the outputs agree with each other and
+with the oracle."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dmmt-jpeg-encoder_amd"))
+sys.path.insert(0, ROOT)
+import dmmt_jpeg  # noqa: E402
+import oracle  # noqa: E402
+from oracle.synth import synthetic  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--w", type=int, default=7680)
+ap.add_argument("--h", type=int, default=4320)
+ap.add_argument("--sub", type=int, default=2)
+ap.add_argument("--q", type=int, default=95)
+ap.add_argument("--frame", type=int, default=95)
+ap.add_argument("--n", type=int, default=4)
+a = ap.parse_args()
+luma, chroma = dmmt_jpeg.quality_tables(a.q)
+opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(a.sub), 8, luma_table=luma,
+                                           chroma_table=chroma)
+rgb = synthetic(a.w, a.h, frame=a.frame)
+enc = dmmt_jpeg.Encoder(0)
+ob = oracle.encode(rgb, 255, a.sub, luma, chroma, threads=8)
+oc = oracle.forward(rgb, 255, a.sub, luma, chroma)
+lib = os.environ.get("DMMT_LIB_PATH", "lib")
+for i in range(a.n):
+    g = enc.encode(dmmt_jpeg.Image.from_array(rgb), opts)
+    gb = enc.encode_coefficients(oc, a.w, a.h, opts)
+    def fd(x):
+        return next((j for j in range(min(len(x), len(ob))) if x[j] != ob[j]), None)
+    print(lib[-30:], i, "whole", g == ob, len(g), fd(g), "back", gb == ob, len(gb), fd(gb), flush=True)
