@@ -686,10 +686,13 @@ extern "C" int dmmt_forward_blocks(dmmt_ctx* c, const dmmt_image* img, const dmm
         StageTimer t(c, ST_FRONT, st);
         HIP_TRY(launch_front(c->in.p, frame_bytes, img->sample_bytes, 1, g, w, st));
     }
-    HIP_TRY(hipMemcpyAsync(coef, w.coef, (size_t)g.bpf * 128, hipMemcpyDeviceToHost, st));
+    std::vector<int16_t> cm((size_t)g.bpf * 64);  // column-major blocks (coef_pos)
+    HIP_TRY(hipMemcpyAsync(cm.data(), w.coef, (size_t)g.bpf * 128, hipMemcpyDeviceToHost, st));
     // the histograms of this partial run are not consumed: clear them
     HIP_TRY(hipMemsetAsync(w.ac_hist, 0, (size_t)kHistReps * 512 * 4, st));
     HIP_TRY(hipStreamSynchronize(st));
+    for (size_t b = 0; b < (size_t)g.bpf; ++b)  // -> zigzag order (frequency_block.rs:26-61)
+        for (int k = 0; k < 64; ++k) coef[b * 64 + k] = cm[b * 64 + coef_pos(k)];
     return take_status(c, st);
 }
 
@@ -709,7 +712,10 @@ extern "C" int dmmt_encode_coefficients(dmmt_ctx* c, const int16_t* coef, size_t
     const size_t out_stride = max_jpeg_bytes(g);
     if ((rc = ensure(c->out, out_stride))) return rc;
     if ((rc = ensure(c->out_len, 4))) return rc;
-    HIP_TRY(hipMemcpyAsync(w.coef, coef, nblocks * 128, hipMemcpyHostToDevice, st));
+    std::vector<int16_t> cm(nblocks * 64);  // zigzag -> column-major blocks (coef_pos)
+    for (size_t b = 0; b < nblocks; ++b)
+        for (int k = 0; k < 64; ++k) cm[b * 64 + coef_pos(k)] = coef[b * 64 + k];
+    HIP_TRY(hipMemcpyAsync(w.coef, cm.data(), nblocks * 128, hipMemcpyHostToDevice, st));
     {
         StageTimer t(c, ST_AC_HIST, st);
         HIP_TRY(launch_ac_hist(1, g, w, st));

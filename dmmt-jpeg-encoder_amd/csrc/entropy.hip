@@ -101,8 +101,28 @@ __device__ __forceinline__ void load_block(const int16_t* __restrict__ p, BlockC
     }
 }
 
+// the coefficient at zigzag position k, after zigzag_in_registers
 __device__ __forceinline__ int coef_at(const BlockCoef& b, int k) {
     return (k & 1) ? ((int)b.w[k >> 1] >> 16) : (int)(int16_t)(b.w[k >> 1] & 0xFFFFu);
+}
+
+// Blocks arrive column-major (coef_pos); the walk wants zigzag order: one
+// constant permutation of the 64 halves in registers, 32 word builds.  (Walking
+// the column-major registers directly, coef_at(b, coef_pos(k)), is the same
+// computation, yet that build produced wrong bits at the head of some blocks on
+// MI355X -- the first block of a wave, nondeterministically; this form is exact
+// on the parity suite.)
+__device__ __forceinline__ void zigzag_in_registers(BlockCoef& b) {
+    uint32_t z[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const int i0 = coef_pos(2 * j), i1 = coef_pos(2 * j + 1);
+        const uint32_t lo = (b.w[i0 >> 1] >> (16 * (i0 & 1))) & 0xFFFFu;
+        const uint32_t hi = (b.w[i1 >> 1] >> (16 * (i1 & 1))) & 0xFFFFu;
+        z[j] = lo | (hi << 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 32; ++j) b.w[j] = z[j];
 }
 
 template <typename Sink>
@@ -279,6 +299,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
             const long long ep = (long long)frame * g.bpf + el0 + p;
             BlockCoef b;
             load_block(coef + ep * 64, b);
+            zigzag_in_registers(b);
             const int dp = dcdiff[ep];
             const int kp = ((int)(el0 % g.bpm) + p) % g.bpm;
             const uint32_t* tp = sTab + (kp < g.n_luma ? 0 : 512);
@@ -337,6 +358,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
                 // occupancy of this kernel
                 BlockCoef b;
                 load_block(coef + e * 64, b);
+                zigzag_in_registers(b);
                 WindowSink ws{sW, w0, wn + 1, 0ull, (int)(start & 31), (int)(start >> 5), true};
                 walk_block(b, dcdiff[e], tb, tb + 256, ws);
                 ws.finish();

@@ -11,6 +11,12 @@ static constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 
                                     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+// Coefficient blocks in HBM are column-major in natural order (k_front stores one
+// 8-coefficient column per lane, 16 bytes): zigzag position k of a block sits at
+// index coef_pos(k) of its 64 int16.  The C ABI's blocks stay in zigzag order
+// (frequency_block.rs), converted on the host.
+constexpr int coef_pos(int k) { return (kZigzag[k] & 7) * 8 + (kZigzag[k] >> 3); }
+
 // Histogram replicas per frame: the front/DC kernels add their per-workgroup
 // histograms into replica (blockIdx.x % kHistReps) to spread atomic traffic.
 static constexpr int kHistReps = 16;

@@ -65,10 +65,7 @@ __device__ __forceinline__ int16_t quantize(float d, float q) {
 // trunc(a + 0.5) there, exactly: a < 2^22 and a's fraction is farther than
 // a * 2^-20 > ulp(a + 0.5) / 2 from 1/2, so the addition cannot round across an
 // integer -- and the rare lanes outside it redone with the division afterwards.
-// out[i] packs rows 2i (low half) and 2i+1 (high half).
-__device__ __forceinline__ void quantize_col8(const float (&v)[8], const float* q, const float* rq,
-                                              uint32_t (&out)[4]) {
-    int x[8];
+__device__ __forceinline__ void quantize_col8(const float (&v)[8], const float* q, const float* rq, int (&x)[8]) {
     bool slow = false;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -86,8 +83,6 @@ __device__ __forceinline__ void quantize_col8(const float (&v)[8], const float* 
                 x[r] = quantize(v[r], q[8 * r]);
         }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
 }
 
 // arai.rs:7-26 constants, f32 literals as written in the reference
@@ -161,8 +156,7 @@ __device__ __forceinline__ void arai8(float (&v)[8]) {
 // NaN (only from 0/0, maxval 0: `nan_possible`) would vanish in the max, so that
 // case always takes the exact path.
 __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const float* q, const float* crq,
-                                                     bool nan_possible, uint32_t (&out)[4]) {
-    int x[8];
+                                                     bool nan_possible, int (&x)[8]) {
     float dist = 0.0f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -178,8 +172,6 @@ __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const 
             if (!(fabsf(t - __builtin_rintf(t)) < 0.4990234375f)) x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
         }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
 }
 
 // color.rs:75-100
@@ -291,12 +283,15 @@ struct RawTile {
 //     luma rows and of the chroma rows in registers -> block-major LDS (stride
 //     BS); with 4:2:x the two threads of a chroma block swap four chroma samples
 //     over DPP and take one chroma row pass each
-//  C  column DCT + quantise (quantize_col8_scaled): one lane per (block, column); results
-//     held in registers across a barrier, then scattered in zigzag order into the
-//     (aliased) int16 block image in local MCU emission order
-//  D  coalesced 16-byte stores of the tile's blocks + DC values (wave 3), beside
-//  E  AC symbols (waves 0-2): two threads per block walk its coefficients from
-//     registers; LDS histogram, flushed once per workgroup.
+//  C  column DCT + quantise (quantize_col8_scaled): one lane per (block, column),
+//     the column's 8 coefficients kept in registers for
+//  D  their store: 16 B per lane, 8 lanes per block (blocks are column-major in
+//     HBM, coef_pos), the DC and the last non-zero position, and
+//  E  the block's AC symbols, counted without a walk: the block's 8 lanes OR their
+//     non-zero bits into its zigzag-order mask (DPP), from which every non-zero
+//     coefficient reads its zero run; LDS histogram, flushed once per workgroup.
+// Two barriers per tile: the next tile's staging barrier also keeps its phase A
+// from overwriting sT before every wave has read its columns.
 template <int HR, int VR, typename Sample, int WPE>
 __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ rgb, size_t frame_stride, Geom g,
                                                const float* __restrict__ norm_lut,
@@ -313,7 +308,6 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     constexpr int NYB = 32 * VR;     // Y blocks: 32 columns x VR rows
     constexpr int CB = TM;           // chroma blocks per component
     constexpr int BS = 72;           // LDS floats per block: 64 + pad (conflict-free column reads)
-    constexpr int CS = 72;           // int16 block stride of the quantised image (144 B: conflict-free 16-B reads)
     constexpr int SP = HR;           // threads per (chroma row, chroma block): one per luma block column
     constexpr int NJ = 8 * CB * SP;  // fused jobs (chroma row, chroma block, luma block column): 256
     constexpr int NCS = 8 / SP;      // chroma samples of a job
@@ -324,19 +318,18 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     constexpr int JPT = (NCJ + 255) / 256;
     using Raw = RawTile<Sample, ROWS>;
 
-    // row-transformed blocks (A..C), then the quantised int16 blocks (C..E)
+    // row-transformed blocks (A -> C)
     __shared__ __attribute__((aligned(16))) float sT[NB * BS];
     __shared__ __attribute__((aligned(16))) uint8_t sRaw[Raw::BYTES];
     // two copies of the AC symbol histograms (luma, chroma), for even and odd
     // blocks: half the same-address collisions of the counting atomics (lanes of
-    // a wave often count the same symbol at the same position); 513 words apart,
-    // so a symbol's two counters sit in different banks
+    // a wave often count the same symbol); 513 words apart, so a symbol's two
+    // counters sit in different banks
     constexpr int HC = 2;
     __shared__ uint32_t sHist[513 * HC];
     __shared__ float sLut[256];
     __shared__ float sQ[128];
     __shared__ float sRQ[128];  // 1/q, correctly rounded; integer samples: fl(scale_row * fl(1/q))
-    int16_t* const sCoef = reinterpret_cast<int16_t*>(sT);
 
     DMMT_TRACE_START;
     const int tid = threadIdx.x;
@@ -347,10 +340,12 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     if (tid < 128) sQ[tid] = qtab[tid];
     if (tid < 128) sRQ[tid] = SB == 4 ? 1.0f / qtab[tid] : c_arai_scale[(tid >> 3) & 7] * (1.0f / qtab[tid]);
     if (SB == 1) sLut[tid] = norm_lut[tid];
-    // the column pass always handles column tid & 7: its 8 zigzag destinations
-    uint8_t zz[8];
+    // the column pass always handles column tid & 7: the zigzag positions of its
+    // 8 coefficients, as the left shift that drops the mask bits from there up
+    const int col = tid & 7;
+    int zsh[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) zz[r] = c_inv_zigzag[r * 8 + (tid & 7)];
+    for (int r = 0; r < 8; ++r) zsh[r] = 64 - (int)c_inv_zigzag[r * 8 + col];
 
     const int tiles_per_row = (g.mcux + TM - 1) / TM;
     const int ntiles = tiles_per_row * g.mcuy;
@@ -512,127 +507,83 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
         DMMT_TRACE(0);
 
         // ---- C: column pass (stride 8, arai.rs:100-102), quantise (quantizer.rs:53-62)
-        uint32_t qv[JPT][4];
+        // ---- D: the tile's blocks in MCU emission order (block_entangler.rs:69-77,
+        //      block_fold_iterator.rs:53-148), only those of MCUs inside the image
+        // ---- E: AC symbols (categorize.rs:132-151): a ZRL per 16 zeros before a
+        //      non-zero, (run & 15) << 4 | category, EOB after trailing zeros
+        const int nvalid = min(TM, g.mcux - mx0) * BPM;
+        const long long e0 = (long long)frame * g.bpf + ((long long)my * g.mcux + mx0) * BPM;
+        static_assert(NCJ % 256 == 0, "whole waves in every column job: the DPP reductions need all lanes");
 #pragma unroll
         for (int jj = 0; jj < JPT; ++jj) {
-            const int job = tid + 256 * jj;
-            if (job < NCJ) {
-                const int col = job & 7, blk = job >> 3;
+            const int blk = (tid + 256 * jj) >> 3;
+            int x[8];
+            {
                 const float* q = sQ + (blk < NYB ? 0 : 64) + col;
+                const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
                 float v[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = sT[blk * BS + i * 8 + col];
-                const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
                 if constexpr (SB == 4) {  // Image<f32> dots: unbounded coefficients
                     arai8(v);
-                    quantize_col8(v, q, rq, qv[jj]);
+                    quantize_col8(v, q, rq, x);
                 } else {
                     arai8_unscaled(v);
-                    quantize_col8_scaled(v, q, rq, g.maxval == 0, qv[jj]);
+                    quantize_col8_scaled(v, q, rq, g.maxval == 0, x);
                 }
             }
-        }
-        __syncthreads();  // every column read: the int16 image may now overwrite sT
-#pragma unroll
-        for (int jj = 0; jj < JPT; ++jj) {
-            const int job = tid + 256 * jj;
-            if (job < NCJ) {
-                const int blk = job >> 3;
-                int el;
-                if (blk < NYB) {
-                    const int by = blk / 32, bx = blk % 32;
-                    el = (bx / HR) * BPM + by * HR + (bx % HR);  // TL,TR,BL,BR (block_entangler.rs:69-77)
-                } else if (blk < NYB + CB) {
-                    el = (blk - NYB) * BPM + NLUMA;
-                } else {
-                    el = (blk - NYB - CB) * BPM + NLUMA + 1;
-                }
-                int16_t* o = sCoef + el * CS;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) o[zz[i]] = (int16_t)(qv[jj][i >> 1] >> (16 * (i & 1)));
+            int el;
+            if (blk < NYB) {
+                const int by = blk / 32, bx = blk % 32;
+                el = (bx / HR) * BPM + by * HR + (bx % HR);  // TL,TR,BL,BR (block_entangler.rs:69-77)
+            } else if (blk < NYB + CB) {
+                el = (blk - NYB) * BPM + NLUMA;
+            } else {
+                el = (blk - NYB - CB) * BPM + NLUMA + 1;
             }
-        }
-        __syncthreads();
-        DMMT_TRACE(2);
-
-        // ---- D + E, side by side: wave 3 stores the tile's blocks (contiguous in
-        // emission order) and DCs; in waves 0-2 two threads per block walk its AC
-        // coefficients from registers and count the run/size symbols
-        // (categorize.rs:132-151): ZRL per 16 zeros before a non-zero, EOB after
-        // trailing zeros.
-        const int nmcu_valid = min(TM, g.mcux - mx0);
-        const int nblk = nmcu_valid * BPM;
-        const long long e0 = (long long)frame * g.bpf + ((long long)my * g.mcux + mx0) * BPM;
-        static_assert(NB <= 96, "two symbol-walk threads per block in waves 0-2");
-        if (tid >= 192) {
-            uint4* dst = reinterpret_cast<uint4*>(coef + e0 * 64);
-            for (int i = tid - 192; i < nblk * 8; i += 64)
-                dst[i] = *reinterpret_cast<const uint4*>(sCoef + (i >> 3) * CS + (i & 7) * 8);
-            for (int b = tid - 192; b < nblk; b += 64) dc[e0 + b] = sCoef[b * CS];
-        } else if (tid < 2 * nblk) {
-            // thread pair per block: half 0 walks zigzag positions 1..31, half 1
-            // positions 32..63 starting from the zero run half 0 ends with
-            const int blk = tid >> 1, half = tid & 1;
-            uint32_t w[16];
-            const uint4* src = reinterpret_cast<const uint4*>(sCoef + blk * CS) + 4 * half;
+            const bool valid = el < nvalid;  // (uniform over the block's 8 lanes)
+            if (valid) {
+                uint32_t pk[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint4 u = src[i];
-                w[4 * i] = u.x;
-                w[4 * i + 1] = u.y;
-                w[4 * i + 2] = u.z;
-                w[4 * i + 3] = u.w;
+                for (int i = 0; i < 4; ++i) pk[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
+                *reinterpret_cast<uint4*>(coef + (e0 + el) * 64 + 8 * col) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
             }
-            // r16 = 16 * (current zero run), so (run & 15) << 4 is r16 & 0xF0 and
-            // run >> 4 is r16 >> 8; ZRLs are summed in a register, counted once
-            // l16 = 16 * (index of the last non-zero + 1), so the zero run before
-            // index kk is 16 * kk - l16 = 16 * run: (run & 15) << 4 is its & 0xF0
-            // and run >> 4 its >> 8; zero positions cost nothing here
-            int l16 = 16;  // half 0: the DC at index 0
-            if (half) {    // the zeros after the last non-zero of positions 1..31 carry over
-                const uint4* lo = reinterpret_cast<const uint4*>(sCoef + blk * CS);
-                uint32_t nzm = 0;  // bit k: position k non-zero
+            // the block's non-zero positions in zigzag order (bit z: position z), over
+            // its 8 lanes; bit 0 (the DC) set, so a run counts from position 1
+            unsigned long long m = 0;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint4 u = lo[i];
-                    const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+            for (int r = 0; r < 8; ++r) m |= (unsigned long long)(x[r] != 0) << (64 - zsh[r]);
+            m |= dpp_u64<0xB1, 0xF, 0xF, false>(m);   // quad_perm [1,0,3,2]: lane ^ 1
+            m |= dpp_u64<0x4E, 0xF, 0xF, false>(m);   // quad_perm [2,3,0,1]: lane ^ 2
+            m |= dpp_u64<0x141, 0xF, 0xF, false>(m);  // row_half_mirror: the other quad
+            m |= 1ull;
+            if (valid) {
+                uint32_t* h = sHist + (blk < NYB ? 0 : 256) + 513 * (blk & 1);
+                uint32_t zrl = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int k = 8 * i + 2 * j;
-                        nzm |= ((q[j] & 0xFFFFu) != 0u ? 1u : 0u) << k;
-                        nzm |= ((q[j] >> 16) != 0u ? 1u : 0u) << (k + 1);
+                for (int r = 0; r < 8; ++r) {
+                    if (x[r] != 0 && zsh[r] != 64) {  // an AC coefficient
+                        // Image<f32> dots only (integer samples bound |v| by 2049): -32768
+                        // has no category (categorize.rs:25-30)
+                        if (SB == 4 && x[r] == -32768) bad |= 4;
+                        const int run = __clzll(m << zsh[r]);  // zeros since the previous non-zero
+                        zrl += (uint32_t)(run >> 4);
+                        atomicAdd(&h[((run & 15) << 4) | category_fast(x[r])], 1u);
                     }
                 }
-                nzm &= ~1u;  // not the DC
-                l16 = -16 * (nzm ? __clz((int)nzm) : 31);
-            }
-            uint32_t* h = sHist + ((blk % BPM) < NLUMA ? 0 : 256) + 513 * (blk % HC);
-            uint32_t zrl = 0;
-#pragma unroll
-            for (int kk = 0; kk < 32; ++kk) {
-                if (kk == 0 && !half) continue;  // the DC
-                const int v = (kk & 1) ? ((int)w[kk >> 1] >> 16) : (int)(int16_t)(w[kk >> 1] & 0xFFFFu);
-                if (v != 0) {
-                    // Image<f32> dots only (integer samples bound |v| by 2049): -32768
-                    // has no category (categorize.rs:25-30)
-                    if (SB == 4 && v == -32768) bad |= 4;
-                    const int r16 = 16 * kk - l16;
-                    if (r16 >= 256) zrl += (uint32_t)(r16 >> 8);  // (rare: a branch, not two VALU ops)
-                    atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
-                    l16 = 16 * kk + 16;
+                if (zrl) atomicAdd(&h[0xF0], zrl);
+                if (col == 0) {
+                    const int last = 63 - __clzll(m);  // 0: no non-zero AC coefficient
+                    if (last < 63) atomicAdd(&h[0], 1u);  // EOB
+                    dc[e0 + el] = (int16_t)x[0];
+                    lastnz[e0 + el] = (uint8_t)last;  // k_emit groups its walks by this
                 }
             }
-            if (zrl) atomicAdd(&h[0xF0], zrl);
-            if (half) {
-                const int r16 = 16 * 32 - l16;  // trailing zeros
-                if (r16) atomicAdd(&h[0], 1u);                     // EOB
-                lastnz[e0 + blk] = (uint8_t)(63 - (r16 >> 4));  // k_emit groups its walks by this
-            }
         }
-        __syncthreads();
-        DMMT_TRACE(4);
+        DMMT_TRACE(2);
     }
 
+    __syncthreads();  // every count in
     if (bad) atomicOr(status, bad);  // 1: sample above maxval, 4: category out of range
     uint32_t* gh = ac_hist + ((size_t)frame * kHistReps + (blockIdx.x % kHistReps)) * 512;
     for (int i = tid; i < 512; i += 256) {
@@ -1088,7 +1039,8 @@ __global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coe
     __syncthreads();
     const long long base = (long long)frame * g.bpf;
     for (long long el = (long long)blockIdx.x * 4 + wave; el < g.bpf; el += (long long)gridDim.x * 4) {
-        const int c = coef[(base + el) * 64 + lane];
+        const int n = c_zigzag[lane];  // lane = zigzag position; blocks are column-major (coef_pos)
+        const int c = coef[(base + el) * 64 + (n & 7) * 8 + (n >> 3)];
         const unsigned long long nz = __ballot(c != 0) & ~1ull;
         if (lane == 0) {
             dc[base + el] = (int16_t)c;
