@@ -155,8 +155,9 @@ __device__ __forceinline__ void arai8(float (&v)[8]) {
 // The eight distances are folded with max (three max3) before one compare; a
 // NaN (only from 0/0, maxval 0: `nan_possible`) would vanish in the max, so that
 // case always takes the exact path.
+// xf[r] = x[r] as f32 (exact), for the symbol's category.
 __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const float* q, const float* crq,
-                                                     bool nan_possible, int (&x)[8]) {
+                                                     bool nan_possible, int (&x)[8], float (&xf)[8]) {
     float dist = 0.0f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -164,12 +165,16 @@ __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const 
         const float n = __builtin_rintf(t);
         dist = fmaxf(dist, fabsf(t - n));
         x[r] = (int)n;
+        xf[r] = n;
     }
     if (nan_possible || !(dist < 0.4990234375f)) {  // 1/2 - 2^-10
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const float t = u[r] * crq[8 * r];
-            if (!(fabsf(t - __builtin_rintf(t)) < 0.4990234375f)) x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
+            if (!(fabsf(t - __builtin_rintf(t)) < 0.4990234375f)) {
+                x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
+                xf[r] = (float)x[r];
+            }
         }
     }
 }
@@ -518,6 +523,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
         for (int jj = 0; jj < JPT; ++jj) {
             const int blk = (tid + 256 * jj) >> 3;
             int x[8];
+            float xf[8];  // x as f32
             {
                 const float* q = sQ + (blk < NYB ? 0 : 64) + col;
                 const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
@@ -527,9 +533,11 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 if constexpr (SB == 4) {  // Image<f32> dots: unbounded coefficients
                     arai8(v);
                     quantize_col8(v, q, rq, x);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) xf[r] = (float)x[r];
                 } else {
                     arai8_unscaled(v);
-                    quantize_col8_scaled(v, q, rq, g.maxval == 0, x);
+                    quantize_col8_scaled(v, q, rq, g.maxval == 0, x, xf);
                 }
             }
             int el;
@@ -568,7 +576,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                         if (SB == 4 && x[r] == -32768) bad |= 4;
                         const int run = __clzll(m << zsh[r]);  // zeros since the previous non-zero
                         zrl += (uint32_t)(run >> 4);
-                        atomicAdd(&h[((run & 15) << 4) | category_fast(x[r])], 1u);
+                        atomicAdd(&h[((run & 15) << 4) | __builtin_amdgcn_frexp_expf(xf[r])], 1u);  // category
                     }
                 }
                 if (zrl) atomicAdd(&h[0xF0], zrl);
