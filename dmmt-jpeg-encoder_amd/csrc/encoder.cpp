@@ -24,7 +24,7 @@ using namespace dmmt;
 
 namespace {
 
-const char* kStageNames[ST_COUNT] = {"front", "dcdiff", "tables", "emit", "offsets", "stuffwrite", "ac_hist"};
+const char* kStageNames[ST_COUNT] = {"front", "hist", "tables", "emit", "offsets", "stuffwrite"};
 
 struct DevBuf {
     void* p = nullptr;
@@ -60,7 +60,7 @@ constexpr int kStatusAsync = 0, kStatusSync = 1;
 struct Lane {
     hipStream_t stream = nullptr;
     DevBuf status;
-    DevBuf coef, dc, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
+    DevBuf coef, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
         chunk_edge, chunk_bit0, chunk_out;
 };
 
@@ -211,7 +211,6 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     const size_t nb = (size_t)g.bpf * nf;
     const size_t nch = (size_t)g.nch * nf;
     if ((rc = ensure(L->coef, nb * 64 * sizeof(int16_t)))) return rc;
-    if ((rc = ensure(L->dc, nb * sizeof(int16_t)))) return rc;
     if ((rc = ensure(L->dcdiff, nb * sizeof(int16_t)))) return rc;
     if ((rc = ensure(L->lastnz, nb))) return rc;
     // staging slots sized for the worst case; k_stuffwrite reads up to 4 words
@@ -231,7 +230,6 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     if ((rc = ensure(L->total_out, (size_t)nf * 8))) return rc;
     if ((rc = ensure(L->status, 16, true))) return rc;
     w->coef = (int16_t*)L->coef.p;
-    w->dc = (int16_t*)L->dc.p;
     w->dcdiff = (int16_t*)L->dcdiff.p;
     w->lastnz = (uint8_t*)L->lastnz.p;
     w->ac_hist = (uint32_t*)L->ac_hist.p;
@@ -312,14 +310,14 @@ struct StageTimer {
     }
 };
 
-// Enqueue the entropy back half (k_dcdiff, k_tables, k_emit, k_offsets,
-// k_stuffwrite) for coefficients already in w.coef / w.dc with AC histograms
-// accumulated.
+// Enqueue the entropy back half (k_hist, k_tables, k_emit, k_offsets,
+// k_stuffwrite) for coefficients already in w.coef.  check_cat: an AC -32768 can
+// occur (Image<f32> input, host blocks).
 int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bits, uint8_t* out, size_t out_stride,
-                      uint32_t* out_len, hipStream_t st, bool dc_done = false) {
-    if (!dc_done) {  // (a stripe's DC differences and counts come from dmmt_stripe_analyze)
-        StageTimer t(c, ST_DCDIFF, st);
-        HIP_TRY(launch_dcdiff(nf, g, w, st));
+                      uint32_t* out_len, hipStream_t st, int check_cat, bool hist_done = false) {
+    if (!hist_done) {  // (a stripe's differences and counts come from dmmt_stripe_analyze)
+        StageTimer t(c, ST_HIST, st);
+        HIP_TRY(launch_hist(nf, g, w, check_cat, st));
     }
     {
         StageTimer t(c, ST_TABLES, st);
@@ -346,7 +344,7 @@ int enqueue_direct(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, 
         StageTimer t(c, ST_FRONT, st);
         HIP_TRY(launch_front(d_rgb, frame_stride, sb, nf, g, w, st));
     }
-    return enqueue_back_half(c, g, nf, w, bits, out, out_stride, out_len, st);
+    return enqueue_back_half(c, g, nf, w, bits, out, out_stride, out_len, st, sb == 4);
 }
 
 void destroy_graphs(dmmt_ctx* c) {
@@ -450,7 +448,7 @@ int set_device(dmmt_ctx* c) { return hip_err(hipSetDevice(c->device)); }
 
 void destroy_lane(Lane* L, bool own_stream) {
     (void)hipStreamSynchronize(L->stream);
-    DevBuf* bufs[] = {&L->status,   &L->coef,      &L->dc,         &L->dcdiff,     &L->lastnz,     &L->ac_hist,
+    DevBuf* bufs[] = {&L->status,   &L->coef,      &L->dcdiff,     &L->lastnz,     &L->ac_hist,
                       &L->dc_hist,  &L->code_tab,  &L->hdr_len,    &L->total_out,  &L->stage,
                       &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out};
     for (DevBuf* b : bufs) release(*b);
@@ -688,8 +686,6 @@ extern "C" int dmmt_forward_blocks(dmmt_ctx* c, const dmmt_image* img, const dmm
     }
     std::vector<int16_t> cm((size_t)g.bpf * 64);  // column-major blocks (coef_pos)
     HIP_TRY(hipMemcpyAsync(cm.data(), w.coef, (size_t)g.bpf * 128, hipMemcpyDeviceToHost, st));
-    // the histograms of this partial run are not consumed: clear them
-    HIP_TRY(hipMemsetAsync(w.ac_hist, 0, (size_t)kHistReps * 512 * 4, st));
     HIP_TRY(hipStreamSynchronize(st));
     for (size_t b = 0; b < (size_t)g.bpf; ++b)  // -> zigzag order (frequency_block.rs:26-61)
         for (int k = 0; k < 64; ++k) coef[b * 64 + k] = cm[b * 64 + coef_pos(k)];
@@ -716,12 +712,8 @@ extern "C" int dmmt_encode_coefficients(dmmt_ctx* c, const int16_t* coef, size_t
     for (size_t b = 0; b < nblocks; ++b)
         for (int k = 0; k < 64; ++k) cm[b * 64 + coef_pos(k)] = coef[b * 64 + k];
     HIP_TRY(hipMemcpyAsync(w.coef, cm.data(), nblocks * 128, hipMemcpyHostToDevice, st));
-    {
-        StageTimer t(c, ST_AC_HIST, st);
-        HIP_TRY(launch_ac_hist(1, g, w, st));
-    }
     if ((rc = enqueue_back_half(c, g, 1, w, opt->bits_per_channel, (uint8_t*)c->out.p, out_stride,
-                                (uint32_t*)c->out_len.p, st)))
+                                (uint32_t*)c->out_len.p, st, 1)))
         return rc;
     uint32_t L = 0;
     HIP_TRY(hipMemcpyAsync(&L, c->out_len.p, 4, hipMemcpyDeviceToHost, st));
@@ -1048,8 +1040,8 @@ extern "C" int dmmt_stripe_analyze(dmmt_ctx* c, const dmmt_stripe* st, const dmm
                              s));
     }
     {
-        StageTimer t(c, ST_DCDIFF, s);
-        HIP_TRY(launch_dcdiff(1, g, w, s));
+        StageTimer t(c, ST_HIST, s);
+        HIP_TRY(launch_hist(1, g, w, st->sample_bytes == 4, s));
     }
     std::vector<uint32_t> ac((size_t)kHistReps * 512), dc((size_t)kHistReps * 32);
     HIP_TRY(hipMemcpyAsync(ac.data(), w.ac_hist, ac.size() * 4, hipMemcpyDeviceToHost, s));
@@ -1071,17 +1063,18 @@ extern "C" int dmmt_stripe_analyze(dmmt_ctx* c, const dmmt_stripe* st, const dmm
         }
     }
     if (g.restart_interval == 0) {  // joined stripes: DC edges for the neighbours' predictors
-        int16_t head[8], tail[8];
-        const int bpm = g.bpm, nl = g.n_luma;
-        HIP_TRY(hipMemcpyAsync(head, w.dc, bpm * sizeof(int16_t), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(tail, w.dc + (g.bpf - bpm), bpm * sizeof(int16_t), hipMemcpyDeviceToHost, s));
+        // the DCs are index 0 of the (column-major) blocks: the first and last MCU
+        std::vector<int16_t> head((size_t)g.bpm * 64), tail((size_t)g.bpm * 64);
+        const int nl = g.n_luma;
+        HIP_TRY(hipMemcpyAsync(head.data(), w.coef, head.size() * 2, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(tail.data(), w.coef + (g.bpf - g.bpm) * 64, tail.size() * 2, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         c->stripe_dc_first[0] = head[0];  // the stripe's first Y, Cb, Cr blocks (emission order)
-        c->stripe_dc_first[1] = head[nl];
-        c->stripe_dc_first[2] = head[nl + 1];
-        c->stripe_dc_last[0] = tail[nl - 1];  // and its last ones
-        c->stripe_dc_last[1] = tail[nl];
-        c->stripe_dc_last[2] = tail[nl + 1];
+        c->stripe_dc_first[1] = head[(size_t)nl * 64];
+        c->stripe_dc_first[2] = head[(size_t)(nl + 1) * 64];
+        c->stripe_dc_last[0] = tail[(size_t)(nl - 1) * 64];  // and its last ones
+        c->stripe_dc_last[1] = tail[(size_t)nl * 64];
+        c->stripe_dc_last[2] = tail[(size_t)(nl + 1) * 64];
     }
     c->stripe_g = g;
     c->stripe_opt = *opt;
@@ -1249,7 +1242,7 @@ extern "C" int dmmt_stripe_encode(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRI
     if ((rc = upload_hist_sum(w, hist_sum, s))) return rc;
     if ((rc = ensure(c->out_len, 4))) return rc;
     if ((rc = enqueue_back_half(c, g, 1, w, c->stripe_opt.bits_per_channel, d_out, out_cap, (uint32_t*)c->out_len.p,
-                                s, true)))
+                                s, 0, true)))
         return rc;
     uint32_t len = 0;
     HIP_TRY(hipMemcpyAsync(&len, c->out_len.p, 4, hipMemcpyDeviceToHost, s));

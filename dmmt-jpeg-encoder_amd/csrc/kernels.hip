@@ -4,13 +4,12 @@
 // or blockIdx.x as noted).  Reference stages in brackets (paths relative to the
 // reference repository):
 //
-//  k_front      pixels -> quantised zigzag blocks in MCU emission order + AC
-//               symbol histograms.  [color.rs:45-100, padder.rs:12-42,
-//               subsampling.rs:102-310, arai.rs:29-104, quantizer.rs:53-62,
-//               block_entangler.rs:5-77, block_fold_iterator.rs:53-148,
-//               categorize.rs:132-151, symbol_counting.rs:55-74]
-//  k_dcdiff     DC prediction in emission order + DC histograms
-//               [categorize.rs:153-169]
+//  k_front      pixels -> quantised blocks in MCU emission order.  [color.rs:45-100,
+//               padder.rs:12-42, subsampling.rs:102-310, arai.rs:29-104,
+//               quantizer.rs:53-62, block_entangler.rs:5-77,
+//               block_fold_iterator.rs:53-148]
+//  k_hist       per block: DC prediction in emission order, AC run/size symbols;
+//               DC and AC histograms [categorize.rs:132-169, symbol_counting.rs:55-74]
 //  k_tables     one workgroup per frame: package-merge code lengths, canonical
 //               codes, JFIF header bytes [symbol_counting.rs:85-94,
 //               length_limited.rs:37-134, huffman/encoder.rs:45-157,
@@ -155,9 +154,8 @@ __device__ __forceinline__ void arai8(float (&v)[8]) {
 // The eight distances are folded with max (three max3) before one compare; a
 // NaN (only from 0/0, maxval 0: `nan_possible`) would vanish in the max, so that
 // case always takes the exact path.
-// xf[r] = x[r] as f32 (exact), for the symbol's category.
 __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const float* q, const float* crq,
-                                                     bool nan_possible, int (&x)[8], float (&xf)[8]) {
+                                                     bool nan_possible, int (&x)[8]) {
     float dist = 0.0f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -165,16 +163,12 @@ __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const 
         const float n = __builtin_rintf(t);
         dist = fmaxf(dist, fabsf(t - n));
         x[r] = (int)n;
-        xf[r] = n;
     }
     if (nan_possible || !(dist < 0.4990234375f)) {  // 1/2 - 2^-10
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const float t = u[r] * crq[8 * r];
-            if (!(fabsf(t - __builtin_rintf(t)) < 0.4990234375f)) {
-                x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
-                xf[r] = (float)x[r];
-            }
+            if (!(fabsf(t - __builtin_rintf(t)) < 0.4990234375f)) x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
         }
     }
 }
@@ -291,20 +285,16 @@ struct RawTile {
 //  C  column DCT + quantise (quantize_col8_scaled): one lane per (block, column),
 //     the column's 8 coefficients kept in registers for
 //  D  their store: 16 B per lane, 8 lanes per block (blocks are column-major in
-//     HBM, coef_pos), the DC and the last non-zero position, and
-//  E  the block's AC symbols, counted without a walk: the block's 8 lanes OR their
-//     non-zero bits into its zigzag-order mask (DPP), from which every non-zero
-//     coefficient reads its zero run; LDS histogram, flushed once per workgroup.
+//     HBM, coef_pos).  The symbols are counted by k_hist, one thread per block:
+//     a walk over the block costs a third of the instructions the same counts
+//     cost here, spread over the block's 8 lanes.
 // Two barriers per tile: the next tile's staging barrier also keeps its phase A
 // from overwriting sT before every wave has read its columns.
 template <int HR, int VR, typename Sample, int WPE>
 __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ rgb, size_t frame_stride, Geom g,
                                                const float* __restrict__ norm_lut,
                                                const float* __restrict__ qtab,  // [2][64] natural, as f32
-                                               int16_t* __restrict__ coef, int16_t* __restrict__ dc,
-                                               uint8_t* __restrict__ lastnz,
-                                               uint32_t* __restrict__ ac_hist,  // [frames][reps][2][256]
-                                               int* __restrict__ status) {
+                                               int16_t* __restrict__ coef, int* __restrict__ status) {
     constexpr int TM = 32 / HR;      // MCUs per tile
     constexpr int ROWS = 8 * VR;     // pixel rows per tile
     constexpr int NLUMA = HR * VR;
@@ -326,12 +316,6 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     // row-transformed blocks (A -> C)
     __shared__ __attribute__((aligned(16))) float sT[NB * BS];
     __shared__ __attribute__((aligned(16))) uint8_t sRaw[Raw::BYTES];
-    // two copies of the AC symbol histograms (luma, chroma), for even and odd
-    // blocks: half the same-address collisions of the counting atomics (lanes of
-    // a wave often count the same symbol); 513 words apart, so a symbol's two
-    // counters sit in different banks
-    constexpr int HC = 2;
-    __shared__ uint32_t sHist[513 * HC];
     __shared__ float sLut[256];
     __shared__ float sQ[128];
     __shared__ float sRQ[128];  // 1/q, correctly rounded; integer samples: fl(scale_row * fl(1/q))
@@ -341,16 +325,10 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     const int frame = blockIdx.y;
     const uint8_t* fbase = reinterpret_cast<const uint8_t*>(rgb + (size_t)frame * frame_stride);
     const long long fbytes = (long long)g.width * g.height * 3 * SB;
-    for (int i = tid; i < 513 * HC; i += 256) sHist[i] = 0;
     if (tid < 128) sQ[tid] = qtab[tid];
     if (tid < 128) sRQ[tid] = SB == 4 ? 1.0f / qtab[tid] : c_arai_scale[(tid >> 3) & 7] * (1.0f / qtab[tid]);
     if (SB == 1) sLut[tid] = norm_lut[tid];
-    // the column pass always handles column tid & 7: the zigzag positions of its
-    // 8 coefficients, as the left shift that drops the mask bits from there up
-    const int col = tid & 7;
-    int zsh[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) zsh[r] = 64 - (int)c_inv_zigzag[r * 8 + col];
+    const int col = tid & 7;  // the column pass always handles column tid & 7
 
     const int tiles_per_row = (g.mcux + TM - 1) / TM;
     const int ntiles = tiles_per_row * g.mcuy;
@@ -514,16 +492,13 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
         // ---- C: column pass (stride 8, arai.rs:100-102), quantise (quantizer.rs:53-62)
         // ---- D: the tile's blocks in MCU emission order (block_entangler.rs:69-77,
         //      block_fold_iterator.rs:53-148), only those of MCUs inside the image
-        // ---- E: AC symbols (categorize.rs:132-151): a ZRL per 16 zeros before a
-        //      non-zero, (run & 15) << 4 | category, EOB after trailing zeros
         const int nvalid = min(TM, g.mcux - mx0) * BPM;
         const long long e0 = (long long)frame * g.bpf + ((long long)my * g.mcux + mx0) * BPM;
-        static_assert(NCJ % 256 == 0, "whole waves in every column job: the DPP reductions need all lanes");
+        static_assert(NCJ % 256 == 0, "JPT column jobs for every thread");
 #pragma unroll
         for (int jj = 0; jj < JPT; ++jj) {
             const int blk = (tid + 256 * jj) >> 3;
             int x[8];
-            float xf[8];  // x as f32
             {
                 const float* q = sQ + (blk < NYB ? 0 : 64) + col;
                 const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
@@ -533,11 +508,9 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 if constexpr (SB == 4) {  // Image<f32> dots: unbounded coefficients
                     arai8(v);
                     quantize_col8(v, q, rq, x);
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) xf[r] = (float)x[r];
                 } else {
                     arai8_unscaled(v);
-                    quantize_col8_scaled(v, q, rq, g.maxval == 0, x, xf);
+                    quantize_col8_scaled(v, q, rq, g.maxval == 0, x);
                 }
             }
             int el;
@@ -556,86 +529,129 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 for (int i = 0; i < 4; ++i) pk[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
                 *reinterpret_cast<uint4*>(coef + (e0 + el) * 64 + 8 * col) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
             }
-            // the block's non-zero positions in zigzag order (bit z: position z), over
-            // its 8 lanes; bit 0 (the DC) set, so a run counts from position 1
-            unsigned long long m = 0;
-#pragma unroll
-            for (int r = 0; r < 8; ++r) m |= (unsigned long long)(x[r] != 0) << (64 - zsh[r]);
-            m |= dpp_u64<0xB1, 0xF, 0xF, false>(m);   // quad_perm [1,0,3,2]: lane ^ 1
-            m |= dpp_u64<0x4E, 0xF, 0xF, false>(m);   // quad_perm [2,3,0,1]: lane ^ 2
-            m |= dpp_u64<0x141, 0xF, 0xF, false>(m);  // row_half_mirror: the other quad
-            m |= 1ull;
-            if (valid) {
-                uint32_t* h = sHist + (blk < NYB ? 0 : 256) + 513 * (blk & 1);
-                uint32_t zrl = 0;
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    if (x[r] != 0 && zsh[r] != 64) {  // an AC coefficient
-                        // Image<f32> dots only (integer samples bound |v| by 2049): -32768
-                        // has no category (categorize.rs:25-30)
-                        if (SB == 4 && x[r] == -32768) bad |= 4;
-                        const int run = __clzll(m << zsh[r]);  // zeros since the previous non-zero
-                        zrl += (uint32_t)(run >> 4);
-                        atomicAdd(&h[((run & 15) << 4) | __builtin_amdgcn_frexp_expf(xf[r])], 1u);  // category
-                    }
-                }
-                if (zrl) atomicAdd(&h[0xF0], zrl);
-                if (col == 0) {
-                    const int last = 63 - __clzll(m);  // 0: no non-zero AC coefficient
-                    if (last < 63) atomicAdd(&h[0], 1u);  // EOB
-                    dc[e0 + el] = (int16_t)x[0];
-                    lastnz[e0 + el] = (uint8_t)last;  // k_emit groups its walks by this
-                }
-            }
         }
         DMMT_TRACE(2);
     }
 
-    __syncthreads();  // every count in
-    if (bad) atomicOr(status, bad);  // 1: sample above maxval, 4: category out of range
-    uint32_t* gh = ac_hist + ((size_t)frame * kHistReps + (blockIdx.x % kHistReps)) * 512;
-    for (int i = tid; i < 512; i += 256) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int c = 0; c < HC; ++c) v += sHist[513 * c + i];
-        if (v) atomicAdd(&gh[i], v);
-    }
+    if (bad) atomicOr(status, bad);  // 1: sample above maxval
     DMMT_TRACE(5);
     DMMT_TRACE_FLUSH(0, 0);
 }
 
-// ============================================================== k_dcdiff
-// DC difference per component in emission order (categorize.rs:153-169), with
-// the predictor reset at restart-interval starts (extension), + DC histograms.
-__global__ __launch_bounds__(256) void k_dcdiff(const int16_t* __restrict__ dc, int16_t* __restrict__ dcdiff, Geom g,
-                                                uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
-                                                int* __restrict__ status) {
-    __shared__ uint32_t sH[32];
+// ============================================================== k_hist
+// One thread per block, emission order (grid-stride over the frame's blocks):
+//  * the DC difference to the previous block of the component (categorize.rs:
+//    153-169; the predictor reset at restart-interval starts, an extension) and
+//    the DC histograms;
+//  * the block's AC symbols (categorize.rs:132-151): a register walk over its 63
+//    AC coefficients in zigzag order -- a ZRL per 16 zeros before a non-zero,
+//    (run & 15) << 4 | category, EOB after trailing zeros -- counted into the AC
+//    histograms (symbol_counting.rs:55-74), and its last non-zero position
+//    (k_emit's walk order).
+// The DC is read from the block itself (index 0 of the column-major block).
+// check_cat: -32768 can occur (Image<f32> dots or host blocks), it has no
+// category (categorize.rs:25-30).
+struct HistCoef {
+    uint32_t w[32];  // zigzag position 2i in the low half of w[i], 2i+1 in the high half
+};
+
+__global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, int16_t* __restrict__ dcdiff,
+                                              uint8_t* __restrict__ lastnz, Geom g, int check_cat,
+                                              uint32_t* __restrict__ ac_hist /*[frames][reps][2][256]*/,
+                                              uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
+                                              int* __restrict__ status) {
+    // four copies of the histograms (lane & 3): the lanes of a wave often count
+    // the same symbol at the same position; 545 words apart (different banks)
+    constexpr int NC = 4, HS = 545;
+    __shared__ uint32_t sH[NC * HS];  // per copy: [AC luma 256][AC chroma 256][DC luma 16][DC chroma 16]
     const int tid = threadIdx.x;
     const int frame = blockIdx.y;
-    if (tid < 32) sH[tid] = 0;
+    for (int i = tid; i < NC * HS; i += 256) sH[i] = 0;
     __syncthreads();
+    uint32_t* const H = sH + HS * (tid & 3);
     const long long base = (long long)frame * g.bpf;
-    bool bad = false;
-    for (long long el = (long long)blockIdx.x * 256 + tid; el < g.bpf; el += (long long)gridDim.x * 256) {
-        const int m = (int)(el / g.bpm);
-        const int k = (int)(el - (long long)m * g.bpm);
-        const bool restart = g.restart_interval > 0 && (m % g.restart_interval) == 0;
-        long long prev = -1;
-        if (k > 0 && k < g.n_luma)
-            prev = el - 1;
-        else if (m > 0 && !restart)
-            prev = (k == 0) ? el - g.bpm + g.n_luma - 1 : el - g.bpm;
-        const int cur = dc[base + el];
-        const int pv = prev >= 0 ? (int)dc[base + prev] : 0;
-        const int16_t d = (int16_t)(cur - pv);  // i16 subtraction
-        bad |= d == -32768;                      // no category (categorize.rs:25-30)
-        dcdiff[base + el] = d;
-        atomicAdd(&sH[(k < g.n_luma ? 0 : 16) + category_of(d)], 1u);
+    const int lane = lane_id();
+    int bad = 0;
+    // block el = MCU m, block k of it (bpf < 2^31: every index fits 32 bits); the
+    // loop steps (m, k) and m mod the restart interval instead of dividing again
+    const uint32_t bpf = (uint32_t)g.bpf, bpm = (uint32_t)g.bpm, ri = (uint32_t)max(g.restart_interval, 1);
+    const uint32_t stride = gridDim.x * 256u, sm = stride / bpm, sk = stride - sm * bpm;
+    uint32_t el = blockIdx.x * 256u + (uint32_t)tid;
+    uint32_t m = el / bpm, k = el - m * bpm, mr = m % ri;
+    const uint32_t smr = sm % ri;
+    for (; el < bpf; el += stride) {
+        const long long e = base + el;
+        const uint4* q = reinterpret_cast<const uint4*>(coef + e * 64);
+        uint32_t cw[32];  // column-major (coef_pos)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint4 v = q[i];
+            cw[4 * i] = v.x, cw[4 * i + 1] = v.y, cw[4 * i + 2] = v.z, cw[4 * i + 3] = v.w;
+        }
+        const int t = k < (uint32_t)g.n_luma ? 0 : 1;
+        // DC: the predictor is the previous block of the component, usually a few
+        // lanes back in this wave (its DC over a lane shuffle), else a load
+        {
+            const bool restart = g.restart_interval > 0 && mr == 0;
+            int back = 0;  // blocks back to the predictor; 0: none (predictor 0)
+            if (k > 0 && k < (uint32_t)g.n_luma)
+                back = 1;
+            else if (m > 0 && !restart)
+                back = (k == 0) ? (int)bpm - g.n_luma + 1 : (int)bpm;
+            const int cur = (int)(int16_t)(cw[0] & 0xFFFFu);
+            const int nb = __shfl_up(cur, (unsigned)back, 64);  // (lanes below `back` get their own)
+            int pv = 0;
+            if (back) pv = lane >= back ? nb : (int)coef[(e - back) * 64];
+            const int16_t d = (int16_t)(cur - pv);  // i16 subtraction
+            bad |= d == -32768 ? 4 : 0;               // no category (categorize.rs:25-30)
+            dcdiff[e] = d;
+            atomicAdd(&H[512 + 16 * t + category_of(d)], 1u);
+        }
+        // AC: zigzag order in registers (a constant permutation of the 64 halves)
+        HistCoef b;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const int i0 = coef_pos(2 * j), i1 = coef_pos(2 * j + 1);
+            const uint32_t lo = (cw[i0 >> 1] >> (16 * (i0 & 1))) & 0xFFFFu;
+            const uint32_t hi = (cw[i1 >> 1] >> (16 * (i1 & 1))) & 0xFFFFu;
+            b.w[j] = lo | (hi << 16);
+        }
+        uint32_t* h = H + 256 * t;
+        // l16 = 16 * (position of the last non-zero + 1): the zero run before position
+        // kk is r16 / 16 with r16 = 16 * kk - l16, (run & 15) << 4 = r16 & 0xF0
+        int l16 = 16;
+        uint32_t zrl = 0;
+#pragma unroll
+        for (int kk = 1; kk < 64; ++kk) {
+            const int v = (kk & 1) ? ((int)b.w[kk >> 1] >> 16) : (int)(int16_t)(b.w[kk >> 1] & 0xFFFFu);
+            if (v != 0) {
+                if (check_cat && v == -32768) bad |= 4;
+                const int r16 = 16 * kk - l16;
+                if (r16 >= 256) zrl += (uint32_t)(r16 >> 8);  // (rare: a branch, not two VALU ops)
+                atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
+                l16 = 16 * kk + 16;
+            }
+        }
+        if (zrl) atomicAdd(&h[0xF0], zrl);
+        if (l16 < 16 * 64) atomicAdd(&h[0], 1u);  // EOB
+        lastnz[e] = (uint8_t)((l16 >> 4) - 1);      // 0: no non-zero AC coefficient
+        m += sm, k += sk, mr += smr;
+        if (k >= bpm) k -= bpm, ++m, ++mr;
+        if (mr >= ri) mr -= ri;
     }
-    if (bad) atomicOr(status, 4);
+    if (bad) atomicOr(status, bad);
     __syncthreads();
-    if (tid < 32 && sH[tid]) atomicAdd(&dc_hist[((size_t)frame * kHistReps + blockIdx.x % kHistReps) * 32 + tid], sH[tid]);
+    const size_t rep = (size_t)frame * kHistReps + blockIdx.x % kHistReps;
+    for (int i = tid; i < 544; i += 256) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v += sH[HS * c + i];
+        if (!v) continue;
+        if (i < 512)
+            atomicAdd(&ac_hist[rep * 512 + i], v);
+        else
+            atomicAdd(&dc_hist[rep * 32 + (i - 512)], v);
+    }
 }
 
 // ============================================================== k_tables
@@ -1033,45 +1049,6 @@ __global__ __launch_bounds__(256) void k_synthetic(uint8_t* __restrict__ rgb, in
 
 }  // namespace dmmt
 
-// ============================================================== standalone AC symbol pass
-// Back-half entry (dmmt_encode_coefficients): blocks come from the host, so the
-// DC values and AC histograms k_front would have produced are rebuilt here.
-namespace dmmt {
-__global__ __launch_bounds__(256) void k_ac_hist(const int16_t* __restrict__ coef, Geom g, int16_t* __restrict__ dc,
-                                                 uint8_t* __restrict__ lastnz, uint32_t* __restrict__ ac_hist,
-                                                 int* __restrict__ status) {
-    __shared__ uint32_t sHist[512];
-    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const int frame = blockIdx.y;
-    for (int i = tid; i < 512; i += 256) sHist[i] = 0;
-    __syncthreads();
-    const long long base = (long long)frame * g.bpf;
-    for (long long el = (long long)blockIdx.x * 4 + wave; el < g.bpf; el += (long long)gridDim.x * 4) {
-        const int n = c_zigzag[lane];  // lane = zigzag position; blocks are column-major (coef_pos)
-        const int c = coef[(base + el) * 64 + (n & 7) * 8 + (n >> 3)];
-        const unsigned long long nz = __ballot(c != 0) & ~1ull;
-        if (lane == 0) {
-            dc[base + el] = (int16_t)c;
-            lastnz[base + el] = (uint8_t)(nz ? 63 - __clzll(nz) : 0);
-        }
-        const int t = (int)(el % g.bpm) < g.n_luma ? 0 : 1;
-        if (lane > 0 && c == -32768) atomicOr(status, 4);  // no category (categorize.rs:25-30)
-        if (lane > 0 && c != 0) {
-            const unsigned long long below = nz & ((1ull << lane) - 1ull);
-            const int p = below ? 63 - __clzll(below) : 0;
-            const int run = lane - p - 1;
-            atomicAdd(&sHist[t * 256 + (((run & 15) << 4) | category_of(c))], 1u);
-            if (run >= 16) atomicAdd(&sHist[t * 256 + 0xF0], (uint32_t)(run >> 4));
-        }
-        if (lane == 63 && c == 0) atomicAdd(&sHist[t * 256], 1u);
-    }
-    __syncthreads();
-    uint32_t* gh = ac_hist + ((size_t)frame * kHistReps + (blockIdx.x % kHistReps)) * 512;
-    for (int i = tid; i < 512; i += 256)
-        if (sHist[i]) atomicAdd(&gh[i], sHist[i]);
-}
-}  // namespace dmmt
-
 // ============================================================== launchers
 namespace dmmt {
 
@@ -1109,7 +1086,7 @@ static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const
     }
     dim3 grid(clampi(ntiles, 1, resident / n_frames > 0 ? resident / n_frames : 1), n_frames);
     hipLaunchKernelGGL((k_front<HR, VR, S, front_wpe<HR, VR, S>()>), grid, dim3(256), 0, st, (const S*)rgb, stride_elems, g, w.norm_lut,
-                       w.qtab, w.coef, w.dc, w.lastnz, w.ac_hist, w.status);
+                       w.qtab, w.coef, w.status);
 }
 
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
@@ -1140,17 +1117,11 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
     return hipGetLastError();
 }
 
-hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
-    dim3 grid(clampi((g.bpf + 3) / 4, 1, 1024 / n_frames > 0 ? 1024 / n_frames : 1), n_frames);
-    hipLaunchKernelGGL(k_ac_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, g, w.dc, w.lastnz, w.ac_hist,
-                       w.status);
-    return hipGetLastError();
-}
-
-hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
+hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st) {
     const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
-    hipLaunchKernelGGL(k_dcdiff, grid, dim3(256), 0, st, (const int16_t*)w.dc, w.dcdiff, g, w.dc_hist, w.status);
+    hipLaunchKernelGGL(k_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g, check_cat,
+                       w.ac_hist, w.dc_hist, w.status);
     return hipGetLastError();
 }
 

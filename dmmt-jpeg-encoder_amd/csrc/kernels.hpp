@@ -10,7 +10,6 @@ namespace dmmt {
 // Device workspace of one launch batch (see the kernels for each buffer's role).
 struct Work {
     int16_t* coef;                  // [frames][bpf][64] zigzag, emission order
-    int16_t* dc;                    // [frames][bpf]
     int16_t* dcdiff;                // [frames][bpf]
     uint8_t* lastnz;                // [frames][bpf] zigzag position of the last non-zero AC (0: none)
     uint32_t* ac_hist;              // [frames][reps][2][256], zero between launches
@@ -30,12 +29,13 @@ struct Work {
     const uint8_t* qtab_u8;         // [2][64]
 };
 
-enum Stage { ST_FRONT = 0, ST_DCDIFF, ST_TABLES, ST_EMIT, ST_OFFSETS, ST_STUFFWRITE, ST_AC_HIST, ST_COUNT };
+enum Stage { ST_FRONT = 0, ST_HIST, ST_TABLES, ST_EMIT, ST_OFFSETS, ST_STUFFWRITE, ST_COUNT };
 
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
                         const Work& w, hipStream_t st);
-hipError_t launch_ac_hist(int n_frames, const Geom& g, const Work& w, hipStream_t st);
-hipError_t launch_dcdiff(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+// DC differences, AC and DC histograms, last non-zero positions of the blocks in
+// w.coef (check_cat: an AC -32768, which has no category, can occur)
+hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st);
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st);
 hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t st);
