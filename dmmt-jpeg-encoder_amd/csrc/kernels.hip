@@ -627,7 +627,7 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
             if (v != 0) {
                 if (check_cat && v == -32768) bad |= 4;
                 const int r16 = 16 * kk - l16;
-                if (r16 >= 256) zrl += (uint32_t)(r16 >> 8);  // (rare: a branch, not two VALU ops)
+                zrl += (uint32_t)(r16 >> 8);
                 atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
                 l16 = 16 * kk + 16;
             }
@@ -1118,7 +1118,7 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 }
 
 hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st) {
-    const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
+    const int per_frame = 4096 / n_frames > 0 ? 4096 / n_frames : 1;  // (8K 4:2:0: 25.3 -> 23.8 us against 1024)
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
     hipLaunchKernelGGL(k_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g, check_cat,
                        w.ac_hist, w.dc_hist, w.status);
