@@ -549,14 +549,16 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
 //    histograms (symbol_counting.rs:55-74), and its last non-zero position
 //    (k_emit's walk order).
 // The DC is read from the block itself (index 0 of the column-major block).
-// check_cat: -32768 can occur (Image<f32> dots or host blocks), it has no
-// category (categorize.rs:25-30).
+// CHECK: an AC -32768 can occur (Image<f32> dots or host blocks); it has no
+// category (categorize.rs:25-30).  Integer samples bound |v| by 2049 and skip the
+// test (four instructions per position of the walk).
 struct HistCoef {
     uint32_t w[32];  // zigzag position 2i in the low half of w[i], 2i+1 in the high half
 };
 
+template <bool CHECK>
 __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, int16_t* __restrict__ dcdiff,
-                                              uint8_t* __restrict__ lastnz, Geom g, int check_cat,
+                                              uint8_t* __restrict__ lastnz, Geom g,
                                               uint32_t* __restrict__ ac_hist /*[frames][reps][2][256]*/,
                                               uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
                                               int* __restrict__ status) {
@@ -625,7 +627,7 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
         for (int kk = 1; kk < 64; ++kk) {
             const int v = (kk & 1) ? ((int)b.w[kk >> 1] >> 16) : (int)(int16_t)(b.w[kk >> 1] & 0xFFFFu);
             if (v != 0) {
-                if (check_cat && v == -32768) bad |= 4;
+                if (CHECK && v == -32768) bad |= 4;
                 const int r16 = 16 * kk - l16;
                 zrl += (uint32_t)(r16 >> 8);
                 atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
@@ -1120,8 +1122,12 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st) {
     const int per_frame = 4096 / n_frames > 0 ? 4096 / n_frames : 1;  // (8K 4:2:0: 25.3 -> 23.8 us against 1024)
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
-    hipLaunchKernelGGL(k_hist, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g, check_cat,
-                       w.ac_hist, w.dc_hist, w.status);
+    if (check_cat)
+        hipLaunchKernelGGL(k_hist<true>, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g,
+                           w.ac_hist, w.dc_hist, w.status);
+    else
+        hipLaunchKernelGGL(k_hist<false>, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g,
+                           w.ac_hist, w.dc_hist, w.status);
     return hipGetLastError();
 }
 
