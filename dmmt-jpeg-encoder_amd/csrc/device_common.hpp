@@ -163,90 +163,16 @@ __device__ __forceinline__ uint32_t extra_bits(int v, int cat) {
     return __builtin_amdgcn_ubfe(p, 0u, (uint32_t)cat);  // width 0 (cat 0) extracts nothing
 }
 
-// Relaxed agent-scope accesses for the look-back status words (gfx950: sc1 loads
-// and stores, bypassing the non-coherent per-CU L1).  Each status word carries
-// its flag and its value in ONE naturally aligned 8-byte word written by ONE
-// store, so a reader that sees the flag sees the value (MI355X_MICROARCH.md
-// "Valid forms", R2 granules).
-__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long lb_load(unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// look-back status word: [63:62] flag (0 none, 1 aggregate, 2 inclusive prefix), [61:0] value
-constexpr unsigned long long kLbAgg = 1ull << 62;
-constexpr unsigned long long kLbPre = 2ull << 62;
-constexpr unsigned long long kLbVal = (1ull << 62) - 1;
-constexpr unsigned kLbSpinLimit = 1u << 22;  // bounded spin: a stuck predecessor sets status bit 4
-
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+// Error report.  `status` points at 8 words of fine-grained (coherent) pinned
+// host memory: error kind k (bit k of `bits`: 0 sample above maxval, 1 Huffman
+// table, 2 category range, 4 output capacity) is word k, set to 1 by a plain
+// vector store -- every writer stores the same value, so concurrent writers need
+// no atomics (none cross PCIe), and the host reads the words after the stream's
+// work without a copy.
+__device__ __forceinline__ void raise_status(int* status, int bits) {
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
-// Decoupled look-back, executed by ONE whole wave: publish `agg` for tile `t`,
-// then read a window of 64 x kLbPerLane predecessor status words per step (all
-// sc1 loads in flight together; lane l holds window positions l*K .. l*K+K-1,
-// position 0 = tile t-1) and stop at the nearest inclusive prefix; if any nearer
-// predecessor has published nothing yet, re-read the window.  Wide windows
-// matter: when many tiles publish their aggregates at the same moment the walk
-// to the nearest prefix is one dependent round trip per window.  Returns the
-// exclusive prefix of tile t (the same value in every lane).  Tiles are handed
-// out by an atomic ticket in the order they start, so every predecessor is
-// already resident and never waits on a successor; the spin is bounded anyway
-// (status bit 4).
-constexpr int kLbPerLane = 16;
-
-__device__ __forceinline__ unsigned long long lookback(unsigned long long* st, unsigned t, unsigned long long agg,
-                                                       int* status) {
-    const int lane = lane_id();
-    if (t == 0) {
-        if (lane == 0) lb_store(&st[0], kLbPre | agg);
-        return 0ull;
-    }
-    if (lane == 0) lb_store(&st[t], kLbAgg | agg);
-    unsigned long long excl = 0;
-    long long j = (long long)t - 1;  // nearest predecessor of the current window
-    unsigned spins = 0;
-    for (;;) {
-        unsigned long long v[kLbPerLane];
-#pragma unroll
-        for (int k = 0; k < kLbPerLane; ++k) {
-            const long long idx = j - (long long)lane * kLbPerLane - k;
-            v[k] = idx >= 0 ? lb_load(&st[idx]) : kLbPre;  // before tile 0: prefix 0
-        }
-        int first_pre = kLbPerLane;  // first inclusive prefix within this lane's run
-        bool none_before = false;    // a "nothing published" word before it
-        unsigned long long part = 0; // values up to and including first_pre
-#pragma unroll
-        for (int k = 0; k < kLbPerLane; ++k) {
-            const unsigned long long flag = v[k] & ~kLbVal;
-            if (first_pre == kLbPerLane) {
-                none_before |= flag == 0;
-                part += v[k] & kLbVal;
-                if (flag == kLbPre) first_pre = k;
-            }
-        }
-        const unsigned long long pre = __ballot(first_pre < kLbPerLane);
-        const int pl = pre ? __ffsll((long long)pre) - 1 : 64;  // lane holding the nearest prefix
-        const bool stall = __any((lane <= pl) && none_before);
-        if (stall) {
-            if (++spins > kLbSpinLimit) {
-                if (lane == 0) atomicOr(status, 4);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        excl += wave_sum_u64(lane <= pl ? part : 0ull);
-        if (pl < 64) break;
-        j -= 64 * kLbPerLane;
-    }
-    if (lane == 0) lb_store(&st[t], kLbPre | (excl + agg));
-    return excl;
+    for (int k = 0; k < 5; ++k)
+        if (bits & (1 << k)) reinterpret_cast<volatile int*>(status)[k] = 1;
 }
 
 }  // namespace dmmt

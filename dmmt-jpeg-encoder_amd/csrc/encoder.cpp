@@ -51,15 +51,20 @@ constexpr size_t kMaxGraphs = 16;
 // One pipeline lane: a device workspace (grown on demand, never shrunk) and the
 // stream that runs on it.  Lane 0 is the context's own stream; dmmt_ctx_set_lanes
 // adds lanes so that consecutive dmmt_encode_device calls overlap.
-// Each lane has its own status words (sticky error bits the kernels OR in):
-// word kStatusAsync collects the asynchronous dmmt_encode_device calls run on the
-// lane and is reported by dmmt_ctx_synchronize; word kStatusSync belongs to the
-// synchronous host calls, which read and clear it before they return.  A host call
-// therefore never reports (or clears) an error of an earlier asynchronous encode.
-constexpr int kStatusAsync = 0, kStatusSync = 1;
+// Each lane has its own status words (sticky error flags the kernels set, one
+// word per error kind, raise_status): group kStatusAsync collects the
+// asynchronous dmmt_encode_device calls run on the lane and is reported by
+// dmmt_ctx_synchronize; group kStatusSync belongs to the synchronous host calls,
+// which read and clear it before they return.  A host call therefore never
+// reports (or clears) an error of an earlier asynchronous encode.  The words live
+// in fine-grained pinned host memory, so reading them after a synchronisation
+// costs no copy (a 4-byte D2H copy per lane took 25-60 us per
+// dmmt_ctx_synchronize).
+constexpr int kStatusAsync = 0, kStatusSync = 1, kStatusWords = 8;
 struct Lane {
     hipStream_t stream = nullptr;
-    DevBuf status;
+    int* status = nullptr;   // [2][kStatusWords], host-mapped
+    int* dstatus = nullptr;  // its device address
     DevBuf coef, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
         chunk_edge, chunk_bit0, chunk_out;
 };
@@ -228,7 +233,17 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     if ((rc = ensure(L->code_tab, (size_t)nf * 1024 * 4))) return rc;
     if ((rc = ensure(L->hdr_len, (size_t)nf * 4))) return rc;
     if ((rc = ensure(L->total_out, (size_t)nf * 8))) return rc;
-    if ((rc = ensure(L->status, 16, true))) return rc;
+    if (!L->status) {
+        void* h = nullptr;
+        HIP_TRY(hipHostMalloc(&h, 2 * kStatusWords * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+        memset(h, 0, 2 * kStatusWords * sizeof(int));
+        L->status = (int*)h;
+        if (hipHostGetDevicePointer((void**)&L->dstatus, h, 0) != hipSuccess) {
+            (void)hipHostFree(h);
+            L->status = nullptr;
+            return DMMT_E_HIP;
+        }
+    }
     w->coef = (int16_t*)L->coef.p;
     w->dcdiff = (int16_t*)L->dcdiff.p;
     w->lastnz = (uint8_t*)L->lastnz.p;
@@ -243,7 +258,7 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     w->chunk_bit0 = (unsigned long long*)L->chunk_bit0.p;
     w->chunk_out = (unsigned long long*)L->chunk_out.p;
     w->total_out = (unsigned long long*)L->total_out.p;
-    w->status = (int*)L->status.p + (async ? kStatusAsync : kStatusSync);
+    w->status = L->dstatus + (async ? kStatusAsync : kStatusSync) * kStatusWords;
     w->norm_lut = nullptr;  // bound by prepare() after upload_tables
     w->qtab = nullptr;
     w->qtab_u8 = nullptr;
@@ -415,17 +430,18 @@ int status_code(int s) {
     return DMMT_OK;
 }
 
-// read and clear one status word of a lane (after the work on `st` that writes it)
-int read_status(Lane* L, int word, hipStream_t st, int* bits) {
+// read and clear one status group of a lane, once the work that writes it is done
+// (st synchronised here; nullptr: the caller has synchronised the device)
+int read_status(Lane* L, int group, hipStream_t st, int* bits) {
     *bits = 0;
-    if (!L->status.p) return DMMT_OK;
-    int* p = (int*)L->status.p + word;
-    HIP_TRY(hipMemcpyAsync(bits, p, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (*bits) {
-        HIP_TRY(hipMemsetAsync(p, 0, sizeof(int), st));
-        HIP_TRY(hipStreamSynchronize(st));
-    }
+    if (!L->status) return DMMT_OK;
+    if (st) HIP_TRY(hipStreamSynchronize(st));
+    volatile int* p = L->status + group * kStatusWords;
+    for (int k = 0; k < kStatusWords; ++k)
+        if (p[k]) {
+            *bits |= 1 << k;
+            p[k] = 0;
+        }
     return DMMT_OK;
 }
 
@@ -437,9 +453,9 @@ int take_status(dmmt_ctx* c, hipStream_t st) {
 }
 
 // fold the asynchronous error bits of a lane (idle: after sync_lanes) into async_bits
-int collect_async(dmmt_ctx* c, Lane* L) {
+int collect_async(dmmt_ctx* c, Lane* L, bool device_synced = false) {
     int s = 0, rc;
-    if ((rc = read_status(L, kStatusAsync, L->stream, &s))) return rc;
+    if ((rc = read_status(L, kStatusAsync, device_synced ? nullptr : L->stream, &s))) return rc;
     c->async_bits |= s;
     return DMMT_OK;
 }
@@ -448,7 +464,8 @@ int set_device(dmmt_ctx* c) { return hip_err(hipSetDevice(c->device)); }
 
 void destroy_lane(Lane* L, bool own_stream) {
     (void)hipStreamSynchronize(L->stream);
-    DevBuf* bufs[] = {&L->status,   &L->coef,      &L->dcdiff,     &L->lastnz,     &L->ac_hist,
+    if (L->status) (void)hipHostFree(L->status);
+    DevBuf* bufs[] = {&L->coef,      &L->dcdiff,     &L->lastnz,     &L->ac_hist,
                       &L->dc_hist,  &L->code_tab,  &L->hdr_len,    &L->total_out,  &L->stage,
                       &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out};
     for (DevBuf* b : bufs) release(*b);
@@ -543,7 +560,7 @@ extern "C" int dmmt_ctx_synchronize(dmmt_ctx* c) {
     if ((rc = set_device(c))) return rc;
     HIP_TRY(hipDeviceSynchronize());
     for (Lane* L : c->lanes)
-        if ((rc = collect_async(c, L))) return rc;
+        if ((rc = collect_async(c, L, true))) return rc;
     const int s = c->async_bits;
     c->async_bits = 0;
     return status_code(s);

@@ -658,7 +658,7 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
     if (end + 2 > out_stride) {  // uniform over the frame
         if (c == 0 && tid == 0) {
             out_len[frame] = 0;  // reported as DMMT_E_CAPACITY by the host
-            atomicOr(status, 16);
+            raise_status(status, 16);
         }
         return;
     }

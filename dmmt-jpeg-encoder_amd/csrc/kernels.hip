@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
         DMMT_TRACE(2);
     }
 
-    if (bad) atomicOr(status, bad);  // 1: sample above maxval
+    if (bad) raise_status(status, bad);  // 1: sample above maxval
     DMMT_TRACE(5);
     DMMT_TRACE_FLUSH(0, 0);
 }
@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
         if (k >= bpm) k -= bpm, ++m, ++mr;
         if (mr >= ri) mr -= ri;
     }
-    if (bad) atomicOr(status, bad);
+    if (bad) raise_status(status, bad);
     __syncthreads();
     const size_t rep = (size_t)frame * kHistReps + blockIdx.x % kHistReps;
     for (int i = tid; i < 544; i += 256) {
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
         for (int w = 0; w < wave; ++w) idx += sCnt[w][tab];
         sKey[idx] = (f << 8) | (unsigned)s;
     }
-    if (sym_thread && ((s == 0 && n == 0) || ((tab & 1) && s == 0xFF && f > 0))) atomicOr(status, 2);
+    if (sym_thread && ((s == 0 && n == 0) || ((tab & 1) && s == 0xFF && f > 0))) raise_status(status, 2);
     __syncthreads();
     DMMT_TRACE(10);
 

@@ -23,7 +23,7 @@ struct Work {
     unsigned long long* chunk_bit0; // [frames][nch] bit offset of the chunk in its restart segment
     unsigned long long* chunk_out;  // [frames][nch] offset of the chunk's output bytes after the header
     unsigned long long* total_out;  // [frames] stuffed scan bytes incl. RST markers
-    int* status;                    // error bits: 1 value>max, 2 table, 4 category range, 16 output capacity
+    int* status;                    // error words (raise_status): bit k of the error kinds -> word k; 1 value>max, 2 table, 4 category range, 16 output capacity
     const float* norm_lut;          // maxval-normalisation table
     const float* qtab;              // [2][64] f32
     const uint8_t* qtab_u8;         // [2][64]
