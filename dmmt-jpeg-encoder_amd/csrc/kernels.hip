@@ -144,16 +144,25 @@ __device__ __forceinline__ void arai8(float (&v)[8]) {
 // most (1/4) * 64 * 128), to within a few ulps; with q >= 1, |d/q| <= 2049 and
 // the saturation of `as i16` cannot trigger.
 // The column pass's output scaling is folded into the reciprocal: u = the
-// unscaled column outputs (arai8_unscaled), crq[8r] = fl(scale_r * fl(1/q)).
-// t = u * crq is within 5 * 2^-24 * 2049 < 2^-10 of the correctly rounded d/q,
-// d = fl(u * scale_r) (five roundings apart), so where t lies farther than 2^-10
-// from a half-integer -- |t - rint(t)| < 1/2 - 2^-10, the difference exact -- both
-// round to the same integer, and as t is then no tie, rint (half to even) is
-// round half away from zero.  The other lanes (and NaN: maxval 0, q 0) redo d and
-// the division afterwards.
-// The eight distances are folded with max (three max3) before one compare; a
-// NaN (only from 0/0, maxval 0: `nan_possible`) would vanish in the max, so that
-// case always takes the exact path.
+// unscaled column outputs (arai8_unscaled, the reference's butterfly values),
+// crq[8r] = fl(scale_r * fl(1/q)).  t = fl(u * crq) and the reference's
+// fl(fl(u * scale_r) / q) are both the exact quotient u * scale_r / q times at
+// most three, resp. two, factors (1 + d), |d| <= 2^-24, so they lie within
+// 5.0001 * 2^-24 * |t| < 2^-21 * |t| of each other.  Where
+// |t - rint(t)| + 2^-21 * |t| < 1/2 the reference's quotient therefore lies in the
+// same open interval (n - 1/2, n + 1/2) around n = rint(t): no tie, and round half
+// away from zero gives n.  Both terms are exact in f32 (Sterbenz; a power-of-two
+// scaling; one fma) and their sum rounds by at most 2^-25, covered by testing against
+// 1/2 - 2^-20.  The margin scales with |t|: small coefficients -- nearly all of
+// them -- take the exact path only within ~|t| * 2^-20 of a half-integer, so a wave
+// almost never has a lane there.  The other lanes (and NaN: maxval 0, q 0) redo d
+// and the division afterwards.
+// The eight distances are folded with max before one compare; a NaN (only from
+// 0/0, maxval 0: `nan_possible`) would vanish in the max, so that case always
+// takes the exact path.
+__device__ __forceinline__ float quant_margin(float t, float n) {
+    return __builtin_fmaf(fabsf(t), 0x1p-21f, fabsf(t - n));  // (the product is exact: one rounding)
+}
 __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const float* q, const float* crq,
                                                      bool nan_possible, int (&x)[8]) {
     float dist = 0.0f;
@@ -161,14 +170,14 @@ __device__ __forceinline__ void quantize_col8_scaled(const float (&u)[8], const 
     for (int r = 0; r < 8; ++r) {
         const float t = u[r] * crq[8 * r];
         const float n = __builtin_rintf(t);
-        dist = fmaxf(dist, fabsf(t - n));
+        dist = fmaxf(dist, quant_margin(t, n));
         x[r] = (int)n;
     }
-    if (nan_possible || !(dist < 0.4990234375f)) {  // 1/2 - 2^-10
+    if (nan_possible || !(dist < 0.49999905f)) {  // 1/2 - 2^-20
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const float t = u[r] * crq[8 * r];
-            if (!(fabsf(t - __builtin_rintf(t)) < 0.4990234375f)) x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
+            if (!(quant_margin(t, __builtin_rintf(t)) < 0.49999905f)) x[r] = quantize(u[r] * c_arai_scale[r], q[8 * r]);
         }
     }
 }
