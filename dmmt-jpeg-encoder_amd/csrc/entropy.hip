@@ -648,7 +648,7 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
                                                     uint8_t* __restrict__ out, size_t out_stride,
                                                     uint32_t* __restrict__ out_len, int* __restrict__ status) {
     __shared__ uint32_t sWave[4];
-    __shared__ uint8_t sOut[2 * kStuffPass];
+    __shared__ __attribute__((aligned(16))) uint8_t sOut[2 * kStuffPass + 16];
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
     const int c = blockIdx.x;
@@ -699,6 +699,9 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
     const unsigned off = (unsigned)(8 * kbeg - b0);  // the first owned byte starts this many bits into the chunk
     uint8_t* o = base + chunk_out[cid];
     for (unsigned long long pos = 0; pos < nbytes; pos += kStuffPass) {  // uniform
+        // the pass is staged at o's alignment (sOut[delta + i] = output byte i), so
+        // it leaves LDS in aligned 16-byte stores
+        const uint32_t delta = (uint32_t)(reinterpret_cast<uintptr_t>(o) & 15u);
         const unsigned long long kb = pos + 16u * (unsigned)tid;          // first of my 16 bytes (chunk-relative)
         const int nvalid = kb < nbytes ? (int)min(16ull, nbytes - kb) : 0;
         uint32_t x[4] = {0u, 0u, 0u, 0u};  // my 16 bytes, MSB first
@@ -734,7 +737,7 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
         // stage the stuffed pass in LDS, then store it with consecutive lanes on
         // consecutive bytes (coalesced)
         if (nvalid) {
-            uint32_t dst = (uint32_t)tid * 16u + pre;
+            uint32_t dst = delta + (uint32_t)tid * 16u + pre;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 if (j < nvalid) {
@@ -747,7 +750,15 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
         __syncthreads();
         const unsigned long long in_pass = nbytes - pos < (unsigned long long)kStuffPass ? nbytes - pos : kStuffPass;
         const uint32_t len = (uint32_t)in_pass + ffs;
-        for (uint32_t i = (uint32_t)tid; i < len; i += 256) o[i] = sOut[i];
+        const uint32_t end = delta + len;  // staged bytes [delta, end)
+        uint8_t* const oa = o - delta;     // 16-byte aligned
+        for (uint32_t b0 = 16u * (uint32_t)tid; b0 < end; b0 += 16u * 256u) {
+            if (b0 >= delta && b0 + 16u <= end) {
+                *reinterpret_cast<uint4*>(oa + b0) = *reinterpret_cast<const uint4*>(sOut + b0);
+            } else {  // the pass's first and last 16-byte pieces: only its own bytes
+                for (uint32_t i = max(b0, delta); i < min(b0 + 16u, end); ++i) oa[i] = sOut[i];
+            }
+        }
         o += len;
         __syncthreads();  // sWave / sOut reuse
     }
