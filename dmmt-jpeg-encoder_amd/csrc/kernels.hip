@@ -503,6 +503,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
         //      block_fold_iterator.rs:53-148), only those of MCUs inside the image
         const int nvalid = min(TM, g.mcux - mx0) * BPM;
         const long long e0 = (long long)frame * g.bpf + ((long long)my * g.mcux + mx0) * BPM;
+        int16_t* const cbase = coef + e0 * 64;  // (uniform: the stores take a 32-bit lane offset)
         static_assert(NCJ % 256 == 0, "JPT column jobs for every thread");
 #pragma unroll
         for (int jj = 0; jj < JPT; ++jj) {
@@ -533,10 +534,10 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
             }
             const bool valid = el < nvalid;  // (uniform over the block's 8 lanes)
             if (valid) {
-                uint32_t pk[4];
+                uint32_t pk[4];  // the low halves of two coefficients per word (one v_perm_b32)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) pk[i] = (uint32_t)(uint16_t)x[2 * i] | ((uint32_t)(uint16_t)x[2 * i + 1] << 16);
-                *reinterpret_cast<uint4*>(coef + (e0 + el) * 64 + 8 * col) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                for (int i = 0; i < 4; ++i) pk[i] = __builtin_amdgcn_perm((uint32_t)x[2 * i + 1], (uint32_t)x[2 * i], 0x05040100u);
+                *reinterpret_cast<uint4*>(cbase + (el * 64 + 8 * col)) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
             }
         }
         DMMT_TRACE(2);
