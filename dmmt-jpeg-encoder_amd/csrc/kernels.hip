@@ -1130,7 +1130,10 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 }
 
 hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st) {
-    const int per_frame = 4096 / n_frames > 0 ? 4096 / n_frames : 1;  // (8K 4:2:0: 25.3 -> 23.8 us against 1024)
+    // at most 1024 workgroups (4K: 1.5 blocks per thread): fewer histogram
+    // flushes; 4K q90 bench 157.5 -> 159.6 Gpx/s, 8K 4:2:0 296.6 -> 299.0 against
+    // one block per thread (512: faster pipelined still, but k_hist alone +4 us)
+    const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
     if (check_cat)
         hipLaunchKernelGGL(k_hist<true>, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g,
