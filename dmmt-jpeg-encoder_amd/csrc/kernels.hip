@@ -10,7 +10,7 @@
 //               block_fold_iterator.rs:53-148]
 //  k_hist       per block: DC prediction in emission order, AC run/size symbols;
 //               DC and AC histograms [categorize.rs:132-169, symbol_counting.rs:55-74]
-//  k_tables     one workgroup per frame: package-merge code lengths, canonical
+//  k_tables     one workgroup per (table, frame): package-merge code lengths, canonical
 //               codes, JFIF header bytes [symbol_counting.rs:85-94,
 //               length_limited.rs:37-134, huffman/encoder.rs:45-157,
 //               encoder.rs:125-262]
