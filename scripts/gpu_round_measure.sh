@@ -19,4 +19,11 @@ for cfg in "4k444q90 --batch 8" "4k444q90 --batch 1" "1080p420q75x256 --batch 64
   timeout -k 10 120 python scripts/e2e_rate.py --config $cfg --seconds 4 >> $O/e2e.jsonl 2>> $O/e2e.err || { echo "e2e $cfg failed"; tail $O/e2e.err; exit 1; }
   tail -1 $O/e2e.jsonl
 done
+# the same at the C ABI, no Python in between (tools/e2e_c, built in-tree beforehand)
+if [ -x tools/e2e_c ]; then
+  for a in "3840 2160 0 90 8 8" "3840 2160 0 90 1 1" "1920 1080 2 75 64 8"; do
+    timeout -k 10 60 ./tools/e2e_c $a 4 >> $O/e2e_c.jsonl 2>> $O/e2e.err || { echo "e2e_c $a failed"; exit 1; }
+    tail -1 $O/e2e_c.jsonl
+  done
+fi
 echo exit=0
