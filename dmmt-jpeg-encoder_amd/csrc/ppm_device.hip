@@ -405,7 +405,8 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
                                                           unsigned long long nsamples, uint32_t maxval) {
     __shared__ uint32_t sWave[kPpmThreads / 64];
     __shared__ unsigned long long sBase;
-    __shared__ Out sOut[kFastChunk / 2];  // at most one token per two bytes
+    // at most one token per two bytes, staged at the output's 16-byte alignment
+    __shared__ __attribute__((aligned(16))) Out sOut[kFastChunk / 2 + 16 / sizeof(Out)];
     if (misc->flag != 0u) return;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
@@ -442,6 +443,9 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
         total += sWave[q];
     }
     uint32_t bad = 0, over = 0;
+    const unsigned long long base = sBase;
+    const uint32_t delta = (uint32_t)((reinterpret_cast<uintptr_t>(out + base) & 15u) / sizeof(Out));
+    slot += delta;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {  // word by word: every register index is static
         uint32_t sj = (uint32_t)(starts >> (4 * j)) & 0xFu;
@@ -461,9 +465,21 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
         } while (sj);
     }
     __syncthreads();
-    const unsigned long long base = sBase;
     const unsigned long long lim = base < nsamples ? min((unsigned long long)total, nsamples - base) : 0ull;
-    for (uint32_t i = tid; i < lim; i += kPpmThreads) out[base + i] = sOut[i];  // consecutive lanes, bytes
+    // aligned 16-byte pieces; the first and last piece only where they hold this
+    // chunk's samples
+    constexpr uint32_t S = sizeof(Out);
+    const uint32_t b_lo = delta * S, b_hi = (delta + (uint32_t)lim) * S;
+    uint8_t* const oa = reinterpret_cast<uint8_t*>(out + base) - b_lo;
+    const uint8_t* const so = reinterpret_cast<const uint8_t*>(sOut);
+    for (uint32_t b0 = 16u * (uint32_t)tid; b0 < b_hi; b0 += 16u * kPpmThreads) {
+        if (b0 >= b_lo && b0 + 16u <= b_hi) {
+            *reinterpret_cast<uint4*>(oa + b0) = *reinterpret_cast<const uint4*>(so + b0);
+        } else {
+            for (uint32_t i = max(b0, b_lo); i < min(b0 + 16u, b_hi); i += S)
+                *reinterpret_cast<Out*>(oa + i) = *reinterpret_cast<const Out*>(so + i);
+        }
+    }
     if (bad) atomicOr(&misc->status_fast, 1u);
     if (over) atomicOr(&misc->status_fast, 2u);
 }
