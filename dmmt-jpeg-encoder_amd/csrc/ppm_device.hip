@@ -14,7 +14,7 @@
 //   k_ppm_count  every chunk's token count (a token starts at each token byte
 //                after whitespace); raises the comment flag on any '#'
 //   k_ppm_carry  one workgroup: exclusive sums of the counts over 1024 rows
-//   k_ppm_fast   every chunk: its tokens parsed from registers (SWAR digits),
+//   k_ppm_fast   every chunk: its tokens parsed token by token (SWAR digits),
 //                staged in LDS in token order, stored coalesced
 //  bodies with comments (flag raised; otherwise these are empty launches), 4 KB
 //  chunks, 16 bytes per thread --
@@ -304,11 +304,12 @@ __device__ __forceinline__ unsigned long long fast_starts(const FastWin& W) {
 //                chunks (or, with comments, the transition-map scan of the
 //                general path)
 //  k_ppm_fast    each chunk: its row's base plus the counts before it in the row,
-//                then its tokens parsed from registers -- walking the window word
-//                by word, a token of at most 4 bytes is one byte-align of two
-//                words, its digits checked and combined per byte lane (SWAR);
-//                longer ones, '+' and bad tokens take the byte walk -- staged in
-//                LDS in token order and stored coalesced
+//                then its tokens parsed token by token (every lane busy until the
+//                wave's largest count; the window's words from LDS) -- a token of
+//                at most 4 bytes is one byte-align of two words, its digits
+//                checked and combined per byte lane (SWAR); longer ones, '+' and
+//                bad tokens take the byte walk -- staged in LDS in token order at
+//                the output's alignment and stored as aligned 16-byte pieces
 // With a '#' anywhere these write nothing that is used: the general kernels
 // (k_ppm_maps, k_ppm_parse) redo the body.
 
@@ -407,6 +408,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
     __shared__ unsigned long long sBase;
     // at most one token per two bytes, staged at the output's 16-byte alignment
     __shared__ __attribute__((aligned(16))) Out sOut[kFastChunk / 2 + 16 / sizeof(Out)];
+    __shared__ uint32_t sWin[kPpmThreads * 17];  // each lane's 16 window words + the next one
     if (misc->flag != 0u) return;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
@@ -446,23 +448,26 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
     const unsigned long long base = sBase;
     const uint32_t delta = (uint32_t)((reinterpret_cast<uintptr_t>(out + base) & 15u) / sizeof(Out));
     slot += delta;
+    uint32_t* const win = sWin + tid * 17;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {  // word by word: every register index is static
-        uint32_t sj = (uint32_t)(starts >> (4 * j)) & 0xFu;
-        if (!sj) continue;
-        const uint32_t lo = F.w[j], hi = j < 15 ? F.w[j + 1] : wn;
-        const uint32_t e8 = j < 15 ? (uint32_t)(ends >> (4 * j)) & 0xFFu
-                                   : ((uint32_t)(ends >> 60) & 0xFu) | (next4 << 4);
-        do {  // at most two tokens start in one word
-            const int r = __builtin_ctz(sj);
-            sj &= sj - 1u;
+    for (int q = 0; q < 16; ++q) win[q] = F.w[q];
+    win[16] = wn;
+    unsigned long long st = starts;
+    while (__any(st != 0ull)) {  // token by token: every lane busy until the wave's largest count
+        if (st) {
+            const int r = __builtin_ctzll(st);
+            st &= st - 1ull;
+            const int j = r >> 2;
+            const uint32_t lo = win[j], hi = win[j + 1];
+            const uint32_t e8 = j < 15 ? (uint32_t)(ends >> (4 * j)) & 0xFFu
+                                       : ((uint32_t)(ends >> 60) & 0xFu) | (next4 << 4);
             bool ok;
-            uint32_t v = fast_token(r, lo, hi, e8, ok);
-            if (!ok) v = parse_token_walk(t, nullptr, 0, pos + 4 * j + r, ok);  // '+', long, not a number
+            uint32_t v = fast_token(r & 3, lo, hi, e8, ok);
+            if (!ok) v = parse_token_walk(t, nullptr, 0, pos + r, ok);  // '+', long, not a number
             bad |= !ok;
             over |= ok && v > maxval;
             sOut[slot++] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
-        } while (sj);
+        }
     }
     __syncthreads();
     const unsigned long long lim = base < nsamples ? min((unsigned long long)total, nsamples - base) : 0ull;
