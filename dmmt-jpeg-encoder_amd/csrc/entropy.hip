@@ -241,16 +241,20 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
                                               uint32_t* __restrict__ stage, uint32_t* __restrict__ chunk_bits,
                                               uint32_t* __restrict__ chunk_ff, uint32_t* __restrict__ chunk_edge,
                                               uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist) {
-    __shared__ uint32_t sTab[4 * 256];
+    // code tables: [luma AC 256][chroma AC 256][luma DC 16][chroma DC 16]
+    __shared__ uint32_t sTab[2 * 256 + 2 * 16];
+    // the window image; during the sort and the walk its first words hold the
+    // walk order, the keys and the blocks' bit counts (read before the window
+    // loop, whose first clear follows two barriers)
     __shared__ uint32_t sW[kEmitWords + 2];
     __shared__ uint32_t sSlot[kSlotWords * 256];
     __shared__ uint32_t sWave[4];
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     __shared__ uint32_t sBin[65];  // walk order: blocks counted, then started, by last non-zero position
-    __shared__ uint8_t sOrder[256];  // block walked by thread u
-    __shared__ uint8_t sKey[256];    // its last non-zero position (ascending in u)
-    __shared__ uint32_t sBits[256];  // bit count of block t
+    uint32_t* const sBits = sW;                                        // [256] bit count of block t
+    uint8_t* const sOrder = reinterpret_cast<uint8_t*>(sW + 256);       // [256] block walked by thread u
+    uint8_t* const sKey = reinterpret_cast<uint8_t*>(sW + 256 + 64);    // [256] its last non-zero position
     DMMT_TRACE_START;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
@@ -260,7 +264,12 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     const int nb = span.nb;
     const long long e = (long long)frame * g.bpf + el0 + tid;
     const size_t cid = (size_t)frame * g.nch + chunk;
-    for (int i = tid; i < 1024; i += 256) sTab[i] = code_tab[(size_t)frame * 1024 + i];
+    {  // code_tab: [luma DC][luma AC][chroma DC][chroma AC] x 256
+        const uint32_t* ct = code_tab + (size_t)frame * 1024;
+        sTab[tid] = ct[256 + tid];
+        sTab[256 + tid] = ct[768 + tid];
+        if (tid < 32) sTab[512 + tid] = ct[(tid < 16 ? 0 : 512 - 16) + tid];
+    }
     if (chunk == 0) {  // the histogram replicas k_tables read: zero for the next launch
         for (int i = tid; i < kHistReps * 512; i += 256) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
         for (int i = tid; i < kHistReps * 32; i += 256) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
@@ -302,18 +311,18 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
             zigzag_in_registers(b);
             const int dp = dcdiff[ep];
             const int kp = ((int)(el0 % g.bpm) + p) % g.bpm;
-            const uint32_t* tp = sTab + (kp < g.n_luma ? 0 : 512);
+            const bool lum = kp < g.n_luma;
             // the wave's walk stops after the last position any of its blocks uses
             const int kmax = __builtin_amdgcn_readfirstlane((int)sKey[min(64 * wave + 63, nb - 1)]);
             SlotSink ss{sSlot + tid, 0ull, 0, 0};
-            walk_block(b, dp, tp, tp + 256, ss, kmax);
+            walk_block(b, dp, sTab + 512 + (lum ? 0 : 16), sTab + (lum ? 0 : 256), ss, kmax);
             sBits[p] = ss.finish();
         }
     }
     __syncthreads();
     const uint32_t bits = valid ? sBits[tid] : 0u;
     const int k = valid ? ((int)(el0 % g.bpm) + tid) % g.bpm : 0;
-    const uint32_t* tb = sTab + (k < g.n_luma ? 0 : 512);
+    const bool lum_t = k < g.n_luma;
     // offsets inside the chunk by a workgroup scan; a block too long for its slot
     // sends the whole chunk down the re-walk path
     const bool over = __syncthreads_or(bits > (uint32_t)kSlotWords * 32u) != 0;
@@ -360,7 +369,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
                 load_block(coef + e * 64, b);
                 zigzag_in_registers(b);
                 WindowSink ws{sW, w0, wn + 1, 0ull, (int)(start & 31), (int)(start >> 5), true};
-                walk_block(b, dcdiff[e], tb, tb + 256, ws);
+                walk_block(b, dcdiff[e], sTab + 512 + (lum_t ? 0 : 16), sTab + (lum_t ? 0 : 256), ws);
                 ws.finish();
             }
         }
