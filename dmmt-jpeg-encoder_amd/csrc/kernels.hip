@@ -602,23 +602,18 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
         }
         const int t = k < (uint32_t)g.n_luma ? 0 : 1;
         // DC: the predictor is the previous block of the component, usually a few
-        // lanes back in this wave (its DC over a lane shuffle), else a load
-        {
-            const bool restart = g.restart_interval > 0 && mr == 0;
-            int back = 0;  // blocks back to the predictor; 0: none (predictor 0)
-            if (k > 0 && k < (uint32_t)g.n_luma)
-                back = 1;
-            else if (m > 0 && !restart)
-                back = (k == 0) ? (int)bpm - g.n_luma + 1 : (int)bpm;
-            const int cur = (int)(int16_t)(cw[0] & 0xFFFFu);
-            const int nb = __shfl_up(cur, (unsigned)back, 64);  // (lanes below `back` get their own)
-            int pv = 0;
-            if (back) pv = lane >= back ? nb : (int)coef[(e - back) * 64];
-            const int16_t d = (int16_t)(cur - pv);  // i16 subtraction
-            bad |= d == -32768 ? 4 : 0;               // no category (categorize.rs:25-30)
-            dcdiff[e] = d;
-            atomicAdd(&H[512 + 16 * t + category_of(d)], 1u);
-        }
+        // lanes back in this wave (its DC over a lane shuffle), else a load -- issued
+        // here, used after the AC walk, so that the walk hides its latency
+        const bool restart = g.restart_interval > 0 && mr == 0;
+        int back = 0;  // blocks back to the predictor; 0: none (predictor 0)
+        if (k > 0 && k < (uint32_t)g.n_luma)
+            back = 1;
+        else if (m > 0 && !restart)
+            back = (k == 0) ? (int)bpm - g.n_luma + 1 : (int)bpm;
+        const int cur = (int)(int16_t)(cw[0] & 0xFFFFu);
+        const int nb = __shfl_up(cur, (unsigned)back, 64);  // (lanes below `back` get their own)
+        int pv = 0;
+        if (back) pv = lane >= back ? nb : (int)coef[(e - back) * 64];
         // AC: zigzag order in registers (a constant permutation of the 64 halves)
         HistCoef b;
 #pragma unroll
@@ -647,6 +642,12 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
         if (zrl) atomicAdd(&h[0xF0], zrl);
         if (l16 < 16 * 64) atomicAdd(&h[0], 1u);  // EOB
         lastnz[e] = (uint8_t)((l16 >> 4) - 1);      // 0: no non-zero AC coefficient
+        {
+            const int16_t d = (int16_t)(cur - pv);  // i16 subtraction
+            bad |= d == -32768 ? 4 : 0;               // no category (categorize.rs:25-30)
+            dcdiff[e] = d;
+            atomicAdd(&H[512 + 16 * t + category_of(d)], 1u);
+        }
         m += sm, k += sk, mr += smr;
         if (k >= bpm) k -= bpm, ++m, ++mr;
         if (mr >= ri) mr -= ri;
