@@ -77,7 +77,12 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
     enc.fill_synthetic_rows(d_in, w, h, y0, y1 - y0, frame=0)
     st = enc.stripe(d_in, w, h, row0, rows)
     cap = enc.stripe_max_bytes(st, opts)
-    d_out = enc.malloc(cap)
+    gather = world > 1 and args.gather
+    if gather:  # a torch buffer: its bytes go to rank 0's file over RCCL (gather_striped)
+        out_t = torch.empty(cap, dtype=torch.uint8, device=torch.device("cuda", local_rank))
+        d_out = out_t.data_ptr()
+    else:
+        d_out = enc.malloc(cap)
     if world == 1 and rpi == 0:
         def step():
             hist = enc.stripe_analyze(st, opts)
@@ -87,6 +92,11 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
         def step():
             hist = enc.stripe_analyze(st, opts)
             return enc.stripe_encode(hist, d_out, cap), 0, None
+    elif gather:
+        def step():
+            n, off, total = dmmt_jpeg.encode_striped(enc, st, opts, d_out, cap)
+            dmmt_jpeg.gather_striped(out_t, n, off, total, root=0)
+            return n, off, total
     else:
         def step():
             return dmmt_jpeg.encode_striped(enc, st, opts, d_out, cap)
@@ -130,7 +140,8 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
                                f"stripe bytes in HBM (histogram all-reduce + size all-gather per step)" if rpi else
                                "no restart intervals (the reference's stream), one MCU-row stripe per GPU joined "
                                "mid-byte, pixels in HBM -> stripe bytes in HBM (edge-DC all-gather, histogram "
-                               "all-reduce, bit-count all-gather, size all-gather per step)"),
+                               "all-reduce, bit-count all-gather, size all-gather per step)")
+                            + ("; the stripes then sent to one file in rank 0's HBM (gather_striped)" if gather else ""),
                 "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
                 "restart_interval": mcux * rpi, "parallelism": f"MCU-row stripes x{world}",
                 "jpeg_bytes": int(total) if total is not None else int(n),
@@ -140,7 +151,8 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
         }
         emit(json.dumps(line))
     enc.free(d_in)
-    enc.free(d_out)
+    if not gather:
+        enc.free(d_out)
     enc.close()
     if world > 1:
         dist.destroy_process_group()
@@ -232,6 +244,8 @@ def main(argv=None, make_encoder=None, emit=None):
     ap.add_argument("--distinct-frames", type=int, default=4)
     ap.add_argument("--ppm-steps", type=int, default=20,
                     help="PPM ingest line: P3 decodes of one synthetic frame timed on rank 0 (0 = skip)")
+    ap.add_argument("--gather", action="store_true",
+                    help="striped configs, N>1: every step also sends the stripes to one file on rank 0 (RCCL p2p)")
     ap.add_argument("--lanes", type=int, default=4,
                     help="pipeline lanes: consecutive steps overlap on this many workspaces/streams (1 = serial)")
     args = ap.parse_args(argv)

@@ -599,6 +599,42 @@ def encode_striped(enc: "Encoder", stripe: DmmtStripe, options: JpegTransformati
     return n, int(sum(sizes[:rank])), int(sum(sizes))
 
 
+def gather_striped(part, n: int, off: int, total: int, root: int = 0, group=None):
+    """The whole JPEG file on rank `root`, from the stripes encode_striped left on
+    the ranks (the stripes concatenated in rank order).  Every rank
+    sends its n bytes point-to-point straight into their place in root's file buffer;
+    with the nccl backend (RCCL) that is a device-to-device copy over xGMI, with
+    gloo the tensors are CPU tensors.  part: uint8 tensor whose first n bytes are
+    this rank's stripe, on the backend's device.  Returns the file (a uint8 tensor
+    of `total` bytes on part's device) on root, None on the other ranks."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if part.dtype != torch.uint8 or part.dim() != 1 or part.numel() < n:
+        raise ValueError("part must be a 1-d uint8 tensor holding at least n bytes")
+    # (n, off) of every stripe: root places each one, the others only send
+    meta = torch.zeros(2 * world, dtype=torch.int64, device=part.device)
+    dist.all_gather_into_tensor(meta, torch.tensor([n, off], dtype=torch.int64, device=part.device), group=group)
+    meta = meta.cpu().view(world, 2).tolist()
+    if sum(m[0] for m in meta) != total or any(meta[r][1] != sum(m[0] for m in meta[:r]) for r in range(world)):
+        raise ValueError("stripe sizes and offsets do not tile the file")
+
+    def peer(r):
+        return dist.get_global_rank(group, r) if group is not None else r
+
+    if rank != root:
+        if n:
+            dist.send(part[:n], dst=peer(root), group=group)
+        return None
+    out = torch.empty(total, dtype=torch.uint8, device=part.device)
+    out[off:off + n].copy_(part[:n])
+    reqs = [dist.irecv(out[o:o + k], src=peer(r), group=group)
+            for r, (k, o) in enumerate(meta) if r != root and k]
+    for q in reqs:
+        q.wait()
+    return out
+
+
 def max_jpeg_bytes(width: int, height: int, subsampling: int) -> int:
     return lib().dmmt_max_jpeg_bytes(width, height, int(subsampling))
 

@@ -187,7 +187,7 @@ def _rank(rank, world, port, out_dir, joined):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "dmmt-jpeg-encoder_amd"))
-    import torch  # noqa: F401
+    import torch
     import torch.distributed as dist
     import dmmt_jpeg as dj
     dist.init_process_group("gloo")
@@ -203,8 +203,14 @@ def _rank(rank, world, port, out_dir, joined):
     cap = enc.stripe_max_bytes(st, opts)
     d_out = enc.malloc(cap)
     n, off, total = dj.encode_striped(enc, st, opts, d_out, cap)
+    mine = enc.d2h(d_out, n)
     with open(os.path.join(out_dir, f"part{rank}.bin"), "wb") as f:
-        f.write(enc.d2h(d_out, n))
+        f.write(mine)
+    # the file assembled on rank 1 (gloo: CPU tensors)
+    whole = dj.gather_striped(torch.frombuffer(bytearray(mine), dtype=torch.uint8), n, off, total, root=1)
+    if whole is not None:
+        with open(os.path.join(out_dir, "file.bin"), "wb") as f:
+            f.write(bytes(whole.tolist()))
     with open(os.path.join(out_dir, f"meta{rank}.json"), "w") as f:
         json.dump({"n": n, "off": off, "total": total}, f)
     enc.free(d_in)
@@ -229,3 +235,4 @@ def test_stripes_two_processes_gloo(tmp_path, joined):
     opts = _opts(2, 75, 0 if joined else 320 // 16)
     assert data == oracle.encode(rgb, 255, 2, opts.luma_table, opts.chroma_table,
                                  restart_interval=opts.restart_interval)
+    assert open(tmp_path / "file.bin", "rb").read() == data  # dmmt_jpeg.gather_striped
