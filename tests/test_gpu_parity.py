@@ -82,6 +82,30 @@ def test_synthetic_shapes(encoder, spec_tables, sub, shape):
 
 
 @pytest.mark.parametrize("sub", SUBS)
+@pytest.mark.parametrize("shape", [(9, 65520), (65520, 9), (1, 65519), (65519, 2)])
+def test_extreme_aspect_at_u16_limit(encoder, spec_tables, sub, shape):
+    """Widths and heights at the u16 limit of Image / PaddedImage (image.rs:7-11,
+    padder.rs:3-9): one MCU row of 4096 MCUs, one MCU column, ragged both ways."""
+    h, w = shape
+    rgb = synthetic(w, h, frame=3)
+    gpu = encoder.encode(dmmt_jpeg.Image.from_array(rgb), opts(sub, *spec_tables))
+    assert gpu == oracle.encode(rgb, 255, sub, *spec_tables)
+
+
+@pytest.mark.parametrize("sub,shape", [(0, (1, 65535)), (2, (65530, 1)), (1, (3, 65535))])
+def test_padded_size_above_u16_is_an_error(encoder, spec_tables, sub, shape):
+    """padder.rs:12-14 computes the padded size in u16; one past 65535 overflows
+    there (a panic in the reference): an error code here, as in the oracle."""
+    h, w = shape
+    rgb = np.zeros((h, w, 3), np.uint8)
+    with pytest.raises(oracle.OracleError) as eo:
+        oracle.encode(rgb, 255, sub, *spec_tables)
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        encoder.encode(dmmt_jpeg.Image.from_array(rgb), opts(sub, *spec_tables))
+    assert e.value.code == eo.value.code == -102
+
+
+@pytest.mark.parametrize("sub", SUBS)
 def test_full_range_noise_all_tables(encoder, presets, sub):
     """uniform noise: large coefficients, long runs of categories, every table."""
     rng = np.random.default_rng(100 + sub)
