@@ -11,7 +11,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["DMMT_LIB_PATH"] = os.path.join(ROOT, "dmmt-jpeg-encoder_amd", "lib_trace", "libdmmt_jpeg.so")
+os.environ["DMMT_LIB_PATH"] = os.path.join(ROOT, "dmmt-jpeg-encoder_amd", os.environ.get("DMMT_TRACE_LIB", "lib_trace"), "libdmmt_jpeg.so")
 sys.path.insert(0, os.path.join(ROOT, "dmmt-jpeg-encoder_amd"))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401
