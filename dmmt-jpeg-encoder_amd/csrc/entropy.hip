@@ -41,13 +41,16 @@ namespace dmmt {
 static __device__ unsigned long long g_trace[64];
 #endif
 
-static_assert(kChunkBlocks == 256, "one thread per block, one workgroup per chunk");
+static_assert(kChunkBlocks == 256 || kChunkBlocks == 512, "one thread per block, one workgroup per chunk");
+constexpr int kEmitThreads = kChunkBlocks;
+constexpr int kEmitWaves = kEmitThreads / 64;
+constexpr int kEmitOcc = kChunkBlocks == 256 ? 7 : 3;  // workgroups per CU
 
 // LDS word window of k_emit: 32 Ki bits = 128 bits per block on average (the 4K
 // q90 workload averages ~110).  A chunk with more is assembled in several
 // windows, every block copying (or, on the re-walk path, re-emitting) only the
 // words inside the window.
-constexpr int kEmitWords = 1024;
+constexpr int kEmitWords = 4 * kChunkBlocks;
 // Bytes per pass of k_stuffwrite (16 per thread).
 constexpr int kStuffPass = 4096;
 
@@ -217,12 +220,12 @@ struct SlotSink {
         if (nacc >= 32) {
             nacc -= 32;
             // past the slot the word lands in its last one: the chunk re-walks then
-            slot[min(wi, kSlotWords - 1) * 256] = (uint32_t)(acc >> nacc);
+            slot[min(wi, kSlotWords - 1) * kEmitThreads] = (uint32_t)(acc >> nacc);
             ++wi;
         }
     }
     __device__ __forceinline__ uint32_t finish() {
-        if (nacc > 0 && wi < kSlotWords) slot[wi * 256] = (uint32_t)(acc << (32 - nacc));
+        if (nacc > 0 && wi < kSlotWords) slot[wi * kEmitThreads] = (uint32_t)(acc << (32 - nacc));
         return (uint32_t)wi * 32u + (uint32_t)nacc;
     }
 };
@@ -235,7 +238,7 @@ __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
 }
 
 // ---------------------------------------------------------------------- k_emit
-__global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
+__global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
                                               const uint8_t* __restrict__ lastnz,
                                               const uint32_t* __restrict__ code_tab, Geom g,
                                               uint32_t* __restrict__ stage, uint32_t* __restrict__ chunk_bits,
@@ -247,14 +250,15 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     // walk order, the keys and the blocks' bit counts (read before the window
     // loop, whose first clear follows two barriers)
     __shared__ uint32_t sW[kEmitWords + 2];
-    __shared__ uint32_t sSlot[kSlotWords * 256];
-    __shared__ uint32_t sWave[4];
+    __shared__ uint32_t sSlot[kSlotWords * kEmitThreads];
+    __shared__ uint32_t sWave[kEmitWaves];
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     __shared__ uint32_t sBin[65];  // walk order: blocks counted, then started, by last non-zero position
-    uint32_t* const sBits = sW;                                        // [256] bit count of block t
-    uint8_t* const sOrder = reinterpret_cast<uint8_t*>(sW + 256);       // [256] block walked by thread u
-    uint8_t* const sKey = reinterpret_cast<uint8_t*>(sW + 256 + 64);    // [256] its last non-zero position
+    using OrderT = std::conditional_t<(kEmitThreads > 256), uint16_t, uint8_t>;
+    uint32_t* const sBits = sW;                                                      // bit count of block t
+    OrderT* const sOrder = reinterpret_cast<OrderT*>(sW + kEmitThreads);               // block walked by thread u
+    uint8_t* const sKey = reinterpret_cast<uint8_t*>(sW + kEmitThreads + kEmitThreads * (int)sizeof(OrderT) / 4);  // its last non-zero position
     DMMT_TRACE_START;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
@@ -266,13 +270,15 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     const size_t cid = (size_t)frame * g.nch + chunk;
     {  // code_tab: [luma DC][luma AC][chroma DC][chroma AC] x 256
         const uint32_t* ct = code_tab + (size_t)frame * 1024;
-        sTab[tid] = ct[256 + tid];
-        sTab[256 + tid] = ct[768 + tid];
+        if (tid < 256) {
+            sTab[tid] = ct[256 + tid];
+            sTab[256 + tid] = ct[768 + tid];
+        }
         if (tid < 32) sTab[512 + tid] = ct[(tid < 16 ? 0 : 512 - 16) + tid];
     }
     if (chunk == 0) {  // the histogram replicas k_tables read: zero for the next launch
-        for (int i = tid; i < kHistReps * 512; i += 256) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
-        for (int i = tid; i < kHistReps * 32; i += 256) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
+        for (int i = tid; i < kHistReps * 512; i += kEmitThreads) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
+        for (int i = tid; i < kHistReps * 32; i += kEmitThreads) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
     }
     if (tid < 8) sFF[tid] = 0u;
     if (tid < 3) sEdge[tid] = 0u;
@@ -296,7 +302,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     __syncthreads();
     const int mine = valid ? (int)(sBin[key] + rank) : tid;
     if (valid) {
-        sOrder[mine] = (uint8_t)tid;
+        sOrder[mine] = (OrderT)tid;
         sKey[mine] = (uint8_t)key;
     }
     __syncthreads();
@@ -330,8 +336,12 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     if (lane == 63) sWave[wave] = incl;
     __syncthreads();
     uint32_t start = incl - bits;
-    for (int q = 0; q < wave; ++q) start += sWave[q];
-    const uint32_t total = sWave[0] + sWave[1] + sWave[2] + sWave[3];
+    uint32_t total = 0;
+#pragma unroll
+    for (int q = 0; q < kEmitWaves; ++q) {
+        start += q < wave ? sWave[q] : 0u;
+        total += sWave[q];
+    }
     DMMT_TRACE(1);
 
     uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
@@ -340,7 +350,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
     uint32_t ff[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int w0 = 0; w0 < nw; w0 += kEmitWords) {  // uniform; one window unless the chunk is huge
         const int wn = min(kEmitWords, nw - w0);
-        for (int i = tid; i <= wn; i += 256) sW[i] = 0u;  // + the next window's first word
+        for (int i = tid; i <= wn; i += kEmitThreads) sW[i] = 0u;  // + the next window's first word
         __syncthreads();
         if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
             if (!over) {
@@ -353,8 +363,8 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
                 const int nsw = (int)((bits + 31) >> 5);
                 for (int d = max(d0, w0); d <= min(d1, w0 + wn); ++d) {
                     const int k = d - d0;  // slot word feeding the low part (k-1 feeds the high part)
-                    const uint32_t lo = k < nsw ? sSlot[k * 256 + mine] : 0u;
-                    const uint32_t hi = k > 0 ? sSlot[(k - 1) * 256 + mine] : 0u;
+                    const uint32_t lo = k < nsw ? sSlot[k * kEmitThreads + mine] : 0u;
+                    const uint32_t hi = k > 0 ? sSlot[(k - 1) * kEmitThreads + mine] : 0u;
                     const uint32_t v = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
                     if (d == d0 || d == d1)
                         atomicOr(&sW[d - w0], v);
@@ -374,7 +384,7 @@ __global__ __launch_bounds__(256, 7) void k_emit(const int16_t* coef, const int1
             }
         }
         __syncthreads();
-        for (int i = tid; i < wn; i += 256) {
+        for (int i = tid; i < wn; i += kEmitThreads) {
             const uint32_t a = sW[i], c = sW[i + 1];
             slot[w0 + i] = a;
             const int wi = w0 + i;
@@ -775,7 +785,7 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
 
 // --------------------------------------------------------------------- launchers
 hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
-    hipLaunchKernelGGL(k_emit, dim3(g.nch, n_frames), dim3(256), 0, st, (const int16_t*)w.coef,
+    hipLaunchKernelGGL(k_emit, dim3(g.nch, n_frames), dim3(kEmitThreads), 0, st, (const int16_t*)w.coef,
                        (const int16_t*)w.dcdiff, (const uint8_t*)w.lastnz, (const uint32_t*)w.code_tab, g, w.stage, w.chunk_bits, w.chunk_ff,
                        w.chunk_edge, w.ac_hist, w.dc_hist);
     return hipGetLastError();

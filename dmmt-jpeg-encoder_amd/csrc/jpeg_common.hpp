@@ -21,7 +21,10 @@ constexpr int coef_pos(int k) { return (kZigzag[k] & 7) * 8 + (kZigzag[k] >> 3);
 // histograms into replica (blockIdx.x % kHistReps) to spread atomic traffic.
 static constexpr int kHistReps = 8;  // (measured: 16 and 4 replicas pipeline 1-2 % slower)
 // Blocks per entropy chunk (k_emit / k_stuffwrite): one workgroup each.
-static constexpr int kChunkBlocks = 256;
+#ifndef DMMT_CHUNK_BLOCKS
+#define DMMT_CHUNK_BLOCKS 256
+#endif
+static constexpr int kChunkBlocks = DMMT_CHUNK_BLOCKS;
 // Worst-case entropy-coded bits of one block: DC code 16 + 12 extra bits, 63 AC
 // tokens of code 16 + 12 extra bits (|coef| <= 2048 for 8-bit-range input).
 static constexpr int kMaxBlockBits = 28 * 64;
