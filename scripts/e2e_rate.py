@@ -13,7 +13,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401  (one HIP runtime per process)
 import dmmt_jpeg  # noqa: E402
 import bench  # noqa: E402
-from oracle.synth import synthetic  # noqa: E402
+import numpy as np  # noqa: E402
 
 
 def main():
@@ -28,7 +28,15 @@ def main():
     opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
                                                chroma_table=chroma)
     enc = dmmt_jpeg.Encoder(0)
-    imgs = [dmmt_jpeg.Image.from_array(synthetic(w, h, frame=f)) for f in range(min(fps, 8))]
+
+    def synthetic(frame):  # the SURVEY 8(d) frames from the library's own device generator
+        d = enc.malloc(w * h * 3)
+        enc.fill_synthetic(d, w, h, 1, first_frame=frame)
+        rgb = np.frombuffer(enc.d2h(d, w * h * 3), np.uint8).reshape(h, w, 3).copy()
+        enc.free(d)
+        return rgb
+
+    imgs = [dmmt_jpeg.Image.from_array(synthetic(f)) for f in range(min(fps, 8))]
     batch = [imgs[i % len(imgs)] for i in range(fps)]
     enc.encode_batch(batch, opts)  # warm-up: workspace, tables
     n, t0 = 0, time.perf_counter()

@@ -2,7 +2,7 @@
 across the option space, each JPEG byte-compared with the oracle.  Extends
 tests/test_gpu_parity.py::test_seeded_random_sweep with larger sizes, Image<f32>
 dots, batches of mixed geometry and pipelined device encodes.
-  python scripts/fuzz_parity.py --cases 5000 --seed 1 [--minutes 5]
+  python tests/tools/fuzz_parity.py --cases 5000 --seed 1 [--minutes 5]
 Prints one JSON line per 250 cases and a summary line; exits 1 on the first
 mismatch (the failing case's parameters in the line)."""
 import argparse
@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dmmt-jpeg-encoder_amd")]
 import dmmt_jpeg  # noqa: E402
 import oracle  # noqa: E402  (checker)
