@@ -44,13 +44,10 @@ def opts(sub, luma, chroma, ri):
     return o
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--cases", type=int, default=5000)
-    ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--minutes", type=float, default=0, help="stop early after this long (0 = no limit)")
-    ap.add_argument("--max-side", type=int, default=1200)
-    args = ap.parse_args()
+def run(cases: int, seed: int, max_side: int = 1200, minutes: float = 0, log=print):
+    """The sweep; returns its summary dict, or the failing case's parameters under
+    "mismatch" (tests/test_gpu_fuzz.py runs a short one in the GPU suite)."""
+    args = argparse.Namespace(cases=cases, seed=seed, max_side=max_side, minutes=minutes)
     rng = np.random.default_rng(args.seed)
     enc = dmmt_jpeg.Encoder(0)
     t0 = time.time()
@@ -122,14 +119,26 @@ def main():
             stats["device"] += lanes * nf
             stats["pixels"] += lanes * nf * h * w
         if not ok:
-            print(json.dumps({"mismatch": params}), flush=True)
-            sys.exit(1)
+            enc.close()
+            return {"mismatch": params}
         done += 1
         if done % 250 == 0:
-            print(json.dumps({"cases": done, "seconds": round(time.time() - t0, 1), **stats}), flush=True)
-    print(json.dumps({"summary": "every JPEG byte-identical to the oracle", "cases": done, "seed": args.seed,
-                      "seconds": round(time.time() - t0, 1), **stats}), flush=True)
+            log(json.dumps({"cases": done, "seconds": round(time.time() - t0, 1), **stats}))
     enc.close()
+    return {"summary": "every JPEG byte-identical to the oracle", "cases": done, "seed": args.seed,
+            "seconds": round(time.time() - t0, 1), **stats}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=5000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--minutes", type=float, default=0, help="stop early after this long (0 = no limit)")
+    ap.add_argument("--max-side", type=int, default=1200)
+    a = ap.parse_args()
+    res = run(a.cases, a.seed, a.max_side, a.minutes, log=lambda line: print(line, flush=True))
+    print(json.dumps(res), flush=True)
+    sys.exit(1 if "mismatch" in res else 0)
 
 
 if __name__ == "__main__":
