@@ -104,16 +104,19 @@ extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) 
     const uint16_t w = hdr.width, h = hdr.height, mx = hdr.maxval;
     const size_t npx = (size_t)w * h;
     const int sb = mx > 255 ? 2 : 1;
-    uint8_t* buf = (uint8_t*)malloc(npx * 3 * (size_t)sb + 1);
+    // The samples a body of this length can hold, at most: a P3 sample takes a
+    // digit and a separator (a success needs all npx * 3 of them), a P6 sample
+    // sb bytes.  A short file claiming a large image allocates no more than that.
+    const size_t body = len - tz.i;
+    const size_t fit = binary ? body / (size_t)sb : body / 2 + 1;
+    if (binary && fit < npx * 3) return DMMT_E_PPM_SIZE_MISMATCH;
+    const size_t cap = npx * 3 < fit ? npx * 3 : fit;
+    uint8_t* buf = (uint8_t*)malloc(cap * (size_t)sb + 1);
     if (!buf) return DMMT_E_OUT_OF_MEMORY;
     if (binary) {
         // P6: exactly one whitespace byte after maxval (already consumed by the
         // tokenizer), then raw big-endian samples.
         const size_t need = npx * 3 * (size_t)sb;
-        if (len - tz.i < need) {
-            free(buf);
-            return DMMT_E_PPM_SIZE_MISMATCH;
-        }
         const uint8_t* s = data + tz.i;
         if (sb == 1) {
             memcpy(buf, s, need);
@@ -131,7 +134,7 @@ extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) 
                 free(buf);
                 return DMMT_E_PPM_PARSE_TOKEN;
             }
-            if (count < npx * 3) {
+            if (count < cap) {
                 if (sb == 1)
                     buf[count] = (uint8_t)(v > 255 ? 255 : v);
                 else
