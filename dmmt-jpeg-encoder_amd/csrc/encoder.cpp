@@ -836,8 +836,14 @@ extern "C" int dmmt_convert_ppm_to_jpeg(dmmt_ctx* c, const char* input_path, con
         hipStream_t st = c->stream;
         const int sb = h.maxval > 255 ? 2 : 1;
         const size_t frame_bytes = (size_t)h.width * h.height * 3 * (size_t)sb;
+        // The decoder writes one sample per token, and a body of n bytes holds at
+        // most n / 2 + 1 tokens (P6: n / sb samples, checked before any write), so
+        // a short file claiming a large image never grows the pooled frame buffer
+        // past what its text can fill; a successful decode needs the whole frame.
+        const size_t body = data.size() - (size_t)h.body_offset;
+        const size_t fit = (h.binary ? body / (size_t)sb : body / 2 + 1) * (size_t)sb;
         if (!(rc = set_device(c)) && !(rc = ensure(c->ppm_text, data.size())) &&
-            !(rc = ensure(c->in, frame_bytes)) &&
+            !(rc = ensure(c->in, std::max<size_t>(std::min(frame_bytes, fit), 16))) &&
             !(rc = hip_err(hipMemcpyAsync(c->ppm_text.p, data.data(), data.size(), hipMemcpyHostToDevice, st))))
             rc = decode_ppm(c, (const uint8_t*)c->ppm_text.p, data.size(), &h, c->in.p, st);
         if (!rc && (h.width == 0 || h.height == 0)) rc = DMMT_E_INVALID_ARGUMENT;  // as check_image

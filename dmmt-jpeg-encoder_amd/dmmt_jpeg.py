@@ -427,8 +427,10 @@ class Encoder:
         h = parse_ppm_header(data)
         n = h.width * h.height * 3
         dt = np.uint8 if h.maxval <= 255 else np.uint16
+        body = len(data) - h.body_offset  # samples the text can fill (as dmmt_convert_ppm_to_jpeg)
+        fit = body // np.dtype(dt).itemsize if h.binary else body // 2 + 1
         d_text = self.malloc(max(len(data), 1))
-        d_rgb = self.malloc(max(n * np.dtype(dt).itemsize, 1))
+        d_rgb = self.malloc(max(min(n, fit) * np.dtype(dt).itemsize, 1))
         try:
             if data:
                 self.h2d(d_text, np.frombuffer(data, np.uint8))

@@ -156,6 +156,29 @@ def test_errors_match_host_reader(encoder, text):
     assert got == code
 
 
+@pytest.mark.parametrize("text", [
+    b"P3 65535 65535 255 1 2 3", b"P3 65535 65535 255 1 2", b"P3 65535 65535 255 1 x 3",
+    b"P3 40000 3 65535 " + b"7 " * 300, b"P6 65535 65535 255\n\x01\x02\x03", b"P6 30000 2 65535\n" + b"\x00" * 10])
+def test_short_body_claiming_a_large_image(encoder, tmp_path, text):
+    """A few bytes of text under a header that claims up to 65535 x 65535: the
+    frame buffer is sized by what the text can fill (a sample per token, a token
+    and a separator per two bytes), never by the header; the error is the host
+    reader's, through the mirror's decode and through convert_ppm_to_jpeg."""
+    code = host_code(text)
+    assert code != 0
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        encoder.read_ppm_device(text)
+    assert e.value.code == code
+    src = tmp_path / "short.ppm"
+    src.write_bytes(text)
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        dmmt_jpeg.convert_ppm_to_jpeg(dmmt_jpeg.Arguments(str(src), str(tmp_path / "o.jpg")))
+    assert e.value.code == code
+    rgb = np.arange(3 * 9 * 5, dtype=np.uint8).reshape(5, 9, 3)  # the context still decodes
+    got, _ = decode_gpu(encoder, b"P6 9 5 255\n" + rgb.tobytes())
+    assert np.array_equal(got, rgb)
+
+
 def test_p6_samples(encoder):
     rgb = np.arange(3 * 5 * 7, dtype=np.uint8).reshape(5, 7, 3)
     got, _ = decode_gpu(encoder, b"P6\n7 5\n255\n" + rgb.tobytes())
