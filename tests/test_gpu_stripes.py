@@ -236,3 +236,34 @@ def test_stripes_two_processes_gloo(tmp_path, joined):
     assert data == oracle.encode(rgb, 255, 2, opts.luma_table, opts.chroma_table,
                                  restart_interval=opts.restart_interval)
     assert open(tmp_path / "file.bin", "rb").read() == data  # dmmt_jpeg.gather_striped
+
+
+def test_seeded_stripe_sweep(encoder):
+    """60 seeded cases of both stripe modes: random size, subsampling, quality,
+    content (noise, flat, 0xFF-rich rows, sparse), stripe count and, in restart
+    mode, interval length; the concatenation must be the oracle's file."""
+    rng = np.random.default_rng(20261017)
+    for case in range(60):
+        sub = int(rng.integers(0, 3))
+        h, w = int(rng.integers(1, 200)), int(rng.integers(1, 200))
+        kind = int(rng.integers(0, 4))
+        if kind == 0:
+            rgb = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        elif kind == 1:
+            rgb = np.full((h, w, 3), int(rng.integers(0, 256)), np.uint8)
+        elif kind == 2:
+            rgb = synthetic(w, h, frame=case)
+            rgb[::int(rng.integers(2, 5))] = 255
+        else:
+            rgb = np.where(rng.random((h, w, 3)) < 0.03, rng.integers(0, 256, (h, w, 3)), 0).astype(np.uint8)
+        q = int(rng.integers(1, 101))
+        mcuy = -(-h // MCU_H[sub])
+        if rng.random() < 0.5:
+            n = int(rng.integers(1, min(mcuy, 8) + 1))
+            data, opts = _joined_on_one_gpu(rgb, sub, q, n)
+        else:
+            rpi = int(rng.integers(1, 4))
+            n = int(rng.integers(1, max(1, min(8, -(-mcuy // rpi))) + 1))
+            data, opts = _striped_on_one_gpu(rgb, sub, q, rpi, n)
+        ref = oracle.encode(rgb, 255, sub, opts.luma_table, opts.chroma_table, restart_interval=opts.restart_interval)
+        assert data == ref, dict(case=case, sub=sub, h=h, w=w, kind=kind, q=q, n=n, ri=opts.restart_interval)
