@@ -6,20 +6,29 @@ tables, bit packing, byte stuffing, headers) over one batch of synthetic frames.
 At N=1 the workload is BASELINE config 2: one 3840x2160 frame, 4:4:4, IJG
 quality 90.  With N GPUs every rank encodes its own frames (independent
 images: weak scaling, no data-path collective); the driver launches one process
-per GPU via torch.distributed.run.
+per GPU via torch.distributed.run, and `--gpus N` without a launcher spawns the
+N rank processes itself (before anything touches a GPU).
 
-Prints ONE JSON line on rank 0.  `value` comes from the timed region (the
-production path: each call replays the cached HIP graph of its seven kernels).
-`roofline` is measured live right after it: HIP events around the dominant
-kernel (k_front) on the stream it is launched on, over the same number of steps
-launched directly.  `cpu_baseline` times the CPU restatement of the reference encoder
-(oracle/, C, the reference's DCT thread-pool structure) on a bounded sample of
-the same workload on this host.
+Prints ONE JSON line on rank 0.  `value` comes from the timed region: the
+production path, every call launched directly (six kernels per frame),
+consecutive frames pipelined over the context's lanes, the input frames rotating
+over enough distinct slots (> 256 MiB together) that their pixels stream from
+HBM rather than the 256 MiB Infinity Cache.  `roofline` comes from a second,
+identical pass with HIP events around every kernel launch, recorded on the
+stream the kernel runs on: per kernel the average launch duration, the
+SURVEY.md 8(d) algorithmic bytes over it, and the PMC traffic from profiles/;
+the dominant (longest) kernel is the headline.  Both passes run the same
+pipelined launches, so `rocprofv3 --kernel-trace --stats` of this command
+averages the same dispatches (profiles/r03_*).  `cpu_baseline` times the CPU
+restatement of the reference encoder (oracle/, C, the reference's DCT
+thread-pool structure) on a bounded sample of the same workload on this host.
 """
 import argparse
 import json
 import os
+import socket
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -33,9 +42,12 @@ import torch.distributed as dist  # noqa: E402
 import dmmt_jpeg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+MALL_BYTES = 256 << 20  # Infinity Cache (MI355X_MICROARCH.md): inputs beyond it stream from HBM
 # f32 VALU issue rate measured on MI355X by tools/pk_rate.hip: 64.2 T lane-ops/s of
 # independent v_add_f32 = 1.003 T wave64 instructions/s over the chip
 VALU_PEAK_PER_S = 1.003e12
+KERNELS = {"front": "k_front", "hist": "k_hist", "tables": "k_tables", "emit": "k_emit", "offsets": "k_offsets",
+           "stuffwrite": "k_stuffwrite"}
 
 CONFIGS = {
     # name: (width, height, subsampling, quality, frames per step)
@@ -48,8 +60,8 @@ CONFIGS = {
 
 
 # one image over all ranks as MCU-row stripes (BASELINE config 4):
-# name: (width, height, subsampling, quality, MCU rows per restart interval)
-STRIPED = {  # (width, height, subsampling, quality, MCU rows per restart interval; 0 = none, joined stripes)
+# name: (width, height, subsampling, quality, MCU rows per restart interval; 0 = none, joined stripes)
+STRIPED = {
     "32k420r": (32768, 32768, 2, 75, 1),
     "32k420": (32768, 32768, 2, 75, 0),
 }
@@ -204,18 +216,55 @@ def ppm_ingest(enc, w, h, steps):
             "algorithmic_bytes": algo, "samples_match": ok}
 
 
-def stage_index(name):
-    L = dmmt_jpeg.lib()
-    for i in range(L.dmmt_num_stages()):
-        if L.dmmt_stage_name(i).decode() == name:
-            return i
-    raise KeyError(name)
+def available_parallelism():
+    """std::thread::available_parallelism() as the reference's CLI default uses it
+    (cli.rs:104-109): the CPUs this process may run on, capped by a cgroup CPU
+    quota.  Returns (that count, nproc, cgroup quota or None)."""
+    nproc = os.cpu_count() or 1
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - not Linux
+        n = nproc
+    quota = None
+    try:  # cgroup v2
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(p))
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // p)
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, quota)
+    return max(1, n), nproc, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# the GPU box's CPU share per GPU: worker pools are sized to it (its nproc shows the
+# whole machine)
+BOX_CPU_SHARE = 16
 
 
 def cpu_baseline(rgb, sub, luma, chroma, budget_s):
-    """Oracle (C restatement, DCT on a thread pool like transformer.rs:126-148) on this host."""
+    """Oracle (C restatement, DCT on a thread pool like transformer.rs:126-148) on this
+    host, with the reference's default thread count (available_parallelism,
+    cli.rs:104-109), at most the GPU box's CPU share."""
     import oracle
-    threads = min(16, os.cpu_count() or 1)
+    avail, nproc, quota = available_parallelism()
+    threads = min(avail, BOX_CPU_SHARE)
     oracle.encode(rgb[:64, :64], 255, sub, luma, chroma)  # load/build
     n = 0
     t0 = time.perf_counter()
@@ -227,9 +276,72 @@ def cpu_baseline(rgb, sub, luma, chroma, budget_s):
     dt = time.perf_counter() - t0
     h, w = rgb.shape[:2]
     return {"value": round(n * w * h / dt / 1e6, 3), "unit": "Mpixel/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "nproc": nproc, "available_parallelism": avail, "cgroup_cpu_quota": quota,
             "sample": f"{n} x {w}x{h} frame(s) of the same synthetic workload, {dt:.1f} s, oracle/cpu_ref.c "
                       f"(C restatement of the reference encoder; DCT on {threads} threads in 700-block jobs, "
-                      f"other stages serial)"}
+                      f"other stages serial, as transformer.rs:126-148; threads = available_parallelism "
+                      f"(the reference's -t default) capped at the box's {BOX_CPU_SHARE}-CPU share)"}
+
+
+def _spawned_rank(rank, argv, world, port, make_encoder, out_dir):
+    """one rank of `bench.py --gpus N` started without a launcher (spawned, so
+    nothing of the parent's process state -- and no GPU -- is inherited)"""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    lines = []
+    main(argv, make_encoder=make_encoder, emit=lines.append)
+    if lines:
+        with open(os.path.join(out_dir, f"rank{rank}.jsonl"), "w") as f:
+            f.write("\n".join(lines) + "\n")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(argv, n, make_encoder, emit):
+    """`--gpus N` with no WORLD_SIZE: start N rank processes (spawn, one per GPU,
+    rendezvous on 127.0.0.1) and emit rank 0's line.  Called before anything here
+    has touched a GPU."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_spawned_rank, args=(argv, n, _free_port(), make_encoder, d), nprocs=n,
+                           start_method="spawn")
+        p = os.path.join(d, "rank0.jsonl")
+        if not os.path.exists(p):
+            raise SystemExit("bench: rank 0 printed no line")
+        for line in open(p).read().splitlines():
+            emit(line)
+
+
+def kernel_roofline(prof, algo_bytes, frames_per_launch, pmc):
+    """per kernel: average launch duration (HIP events on its stream), the SURVEY
+    8(d) algorithmic bytes of the frames one launch processes over it, and the PMC
+    traffic / instruction counts of profiles/pmc_<config>.json"""
+    out = {}
+    for stage, name in KERNELS.items():
+        ms, n = prof.get(stage, (0.0, 0))
+        if not n:
+            continue
+        avg_s = ms / 1e3 / n
+        achieved = algo_bytes / avg_s / 1e9
+        k = {"avg_launch_us": round(avg_s * 1e6, 2), "launches": n, "achieved": round(achieved, 1),
+             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
+        pk = (pmc or {}).get("kernels", {}).get(name)
+        if pk:
+            if pk.get("hbm_bytes") is not None:
+                k["traffic"] = round(pk["hbm_bytes"])
+            if pk.get("SQ_INSTS_VALU") is not None:
+                k["valu_wave_insts"] = round(pk["SQ_INSTS_VALU"])
+                k["valu_frac"] = round(pk["SQ_INSTS_VALU"] / avg_s / VALU_PEAK_PER_S, 4)
+            if pk.get("SQ_INSTS_SALU") is not None:
+                k["salu_wave_insts"] = round(pk["SQ_INSTS_SALU"])
+            if pk.get("SQ_WAIT_ANY") and pk.get("SQ_WAVE_CYCLES"):
+                k["parked_frac"] = round(pk["SQ_WAIT_ANY"] / pk["SQ_WAVE_CYCLES"], 3)
+        out[name] = k
+    return out
 
 
 def main(argv=None, make_encoder=None, emit=None):
@@ -241,7 +353,12 @@ def main(argv=None, make_encoder=None, emit=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="4k444q90", choices=sorted(CONFIGS) + sorted(STRIPED))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
-    ap.add_argument("--distinct-frames", type=int, default=4)
+    ap.add_argument("--distinct-frames", type=int, default=0,
+                    help="input slots the steps rotate over (0 = enough to exceed the 256 MiB Infinity Cache)")
+    ap.add_argument("--mall-compare", action="store_true",
+                    help="also time the steps over 4 input slots (inputs resident in the Infinity Cache)")
+    ap.add_argument("--latency", action="store_true",
+                    help="also time the steps one at a time (one lane): the latency of one frame")
     ap.add_argument("--ppm-steps", type=int, default=20,
                     help="PPM ingest line: P3 decodes of one synthetic frame timed on rank 0 (0 = skip)")
     ap.add_argument("--gather", action="store_true",
@@ -249,12 +366,16 @@ def main(argv=None, make_encoder=None, emit=None):
     ap.add_argument("--lanes", type=int, default=4,
                     help="pipeline lanes: consecutive steps overlap on this many workspaces/streams (1 = serial)")
     args = ap.parse_args(argv)
-    make_encoder = make_encoder or dmmt_jpeg.Encoder
     emit = emit or (lambda line: print(line, flush=True))
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # no launcher: start the ranks here
+        return spawn_ranks(list(argv if argv is not None else sys.argv[1:]), args.gpus, make_encoder, emit)
+    make_encoder = make_encoder or dmmt_jpeg.Encoder
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a wrong n_gpus")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -280,53 +401,54 @@ def main(argv=None, make_encoder=None, emit=None):
     opt_c = opts.to_c()
     enc = make_encoder(local_rank)
 
-    nslots = max(1, args.distinct_frames)
     frame_bytes = w * h * 3
+    slot_bytes = frame_bytes * fps
+    # distinct input slots: enough that between two reads of a slot more than the
+    # Infinity Cache's capacity of other frames has streamed past (4K: 13 x 24.9 MB)
+    nslots = args.distinct_frames if args.distinct_frames > 0 else max(4, MALL_BYTES // slot_bytes + 2)
     out_stride = (dmmt_jpeg.max_jpeg_bytes(w, h, sub) + 255) // 256 * 256
     lanes = max(1, args.lanes)
-    d_in = [enc.malloc(frame_bytes * fps) for _ in range(nslots)]
+    d_in = [enc.malloc(slot_bytes) for _ in range(nslots)]
     d_out = [enc.malloc(out_stride * fps) for _ in range(lanes)]  # one per lane: never shared by concurrent steps
     d_len = [enc.malloc(4 * fps) for _ in range(lanes)]
     for s in range(nslots):  # distinct synthetic frames per slot and per rank
         enc.fill_synthetic(d_in[s], w, h, fps, first_frame=(rank * nslots + s) * fps)
 
-    def step(i, nl):
-        enc.encode_device(d_in[i % nslots], fps, w, h, None, d_out[i % nl], out_stride, d_len[i % nl],
+    def step(i, nl, ns):
+        enc.encode_device(d_in[i % ns], fps, w, h, None, d_out[i % nl], out_stride, d_len[i % nl],
                           frame_stride=frame_bytes, opt_c=opt_c)
 
-    def timed(nl):
+    def timed(nl, ns=nslots):
         enc.set_lanes(nl)
         for i in range(args.warmup):
-            step(i, nl)
+            step(i, nl, ns)
         barrier_sync(enc)
         barrier_sync(enc)
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(i, nl)
+            step(i, nl, ns)
         barrier_sync(enc)
         return time.perf_counter() - t0
 
     # timed region: the production path (no event timing inside); with lanes > 1
     # consecutive frames are pipelined over the context's lanes (dmmt_ctx_set_lanes)
     elapsed = timed(lanes)
-    # the same steps one at a time (one lane): the latency of one frame
-    single = timed(1) if lanes > 1 else elapsed
-
-    # roofline pass: the same steps again, one lane, with HIP events around k_front
-    # on the stream it runs on
-    front = stage_index("front")
-    enc.set_profiling(1 << front)
-    barrier_sync(enc)
-    for i in range(args.steps):
-        step(i, 1)
-    barrier_sync(enc)
+    # roofline pass: the same pipelined steps again with HIP events around every
+    # kernel launch, on the stream it is launched on
+    enc.set_profiling(1)
+    timed(lanes)
     prof = enc.profile()
     enc.set_profiling(0)
+    extra = {}
+    if args.mall_compare:  # inputs resident in the Infinity Cache: 4 slots
+        extra["mall_resident_4_slots"] = timed(lanes, min(4, nslots))
+    if args.latency and lanes > 1:  # the same steps one at a time: the latency of one frame
+        extra["single_lane"] = timed(1)
 
     if world > 1:
-        t = torch.tensor([elapsed, single], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, single = (float(x) for x in t.tolist())
+        elapsed = float(t.item())
 
     lens = np.frombuffer(enc.d2h(d_len[0], 4 * fps), np.uint32)
     jpeg_bytes = float(lens.mean())
@@ -334,39 +456,41 @@ def main(argv=None, make_encoder=None, emit=None):
     if rank == 0:
         pixels = w * h * fps * args.steps * world
         value = pixels / elapsed / 1e6
-        front_ms, front_n = prof["front"]
-        avg_front_s = front_ms / 1e3 / max(front_n, 1)
-        # the path's algorithmic bytes are 3 B/px of RGB in + the
-        # JPEG bytes out; k_front's share is the RGB it reads (the quantised
-        # coefficients it writes are intermediate traffic, counted in `traffic`)
-        algo_bytes = fps * w * h * 3
-        achieved = algo_bytes / avg_front_s / 1e9
-        path_bytes = algo_bytes + fps * jpeg_bytes
-        path_achieved = path_bytes / (elapsed / args.steps) / 1e9
-        traffic = None
-        valu = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-        if os.path.exists(pmc):
+        # the path's algorithmic bytes per frame are 3 B/px of RGB in
+        # + the JPEG bytes out; a launch processes `fps` frames
+        algo_bytes = fps * (w * h * 3 + jpeg_bytes)
+        path_achieved = algo_bytes / (elapsed / args.steps) / 1e9
+        pmc = None
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if os.path.exists(pmc_path):
             try:
-                pmc_d = json.load(open(pmc))
-                traffic = pmc_d.get("front_hbm_bytes_per_launch")
-                n_valu = pmc_d["kernels"]["k_front"].get("SQ_INSTS_VALU")
-                if n_valu:
-                    # the bound that does apply: VALU wave-instructions
-                    # per launch (PMC) / this launch time, against the issue rate
-                    # tools/pk_rate.hip measured (independent v_add_f32 streams)
-                    rate = n_valu / avg_front_s
-                    valu = {"wave_instructions_per_launch": round(n_valu), "achieved_per_s": round(rate, -6),
-                            "peak_per_s": VALU_PEAK_PER_S, "frac": round(rate / VALU_PEAK_PER_S, 4),
-                            "source": f"profiles/pmc_{args.config}.json SQ_INSTS_VALU; peak tools/pk_rate.hip"}
-            except Exception:
-                traffic = valu = None
+                pmc = json.load(open(pmc_path))
+            except ValueError:
+                pmc = None
+        kern = kernel_roofline(prof, algo_bytes, fps, pmc)
+        dom = max(kern, key=lambda k: kern[k]["avg_launch_us"]) if kern else None
+        d = kern.get(dom, {})
         ingest = ppm_ingest(enc, w, h, args.ppm_steps) if args.ppm_steps > 0 else None
         cpu = None
         if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
             from oracle.synth import synthetic  # numpy twin of the device generator
             rgb = synthetic(w, h, frame=0)
             cpu = cpu_baseline(rgb, sub, luma, chroma, args.cpu_seconds)
+        cfg = {
+            "workload": f"{w}x{h} synthetic RGB u8, {['4:4:4', '4:2:2', '4:2:0'][sub]}, IJG quality {quality}, "
+                        f"{fps} frame(s) per step per GPU, pixels in HBM -> JPEG files in HBM, inputs rotating "
+                        f"over {nslots} distinct slots ({nslots * slot_bytes / 2**20:.0f} MiB: streamed from HBM)",
+            "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
+            "frames_per_step": fps, "mean_jpeg_bytes": jpeg_bytes, "parallelism": f"independent frames x{world}",
+            "lanes": lanes, "input_slots": nslots,
+        }
+        if "mall_resident_4_slots" in extra:
+            t4 = extra["mall_resident_4_slots"]
+            cfg["mall_resident_4_slots_value"] = round(pixels / world / t4 / 1e6, 2)
+        if "single_lane" in extra:
+            t1 = extra["single_lane"]
+            cfg["single_lane_ms_per_step"] = round(t1 / args.steps * 1e3, 4)
+            cfg["single_lane_value"] = round(pixels / world / t1 / 1e6, 2)
         line = {
             "metric": "Mpixel/s encoded (4K PPM, q=90)" if args.config == "4k444q90" else f"Mpixel/s encoded ({args.config})",
             "value": round(value, 2),
@@ -380,28 +504,26 @@ def main(argv=None, make_encoder=None, emit=None):
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {
-                "workload": f"{w}x{h} synthetic RGB u8, {['4:4:4', '4:2:2', '4:2:0'][sub]}, IJG quality {quality}, "
-                            f"{fps} frame(s) per step per GPU, pixels in HBM -> JPEG files in HBM",
-                "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
-                "frames_per_step": fps, "mean_jpeg_bytes": jpeg_bytes, "parallelism": f"independent frames x{world}",
-                "lanes": lanes,
-                "single_lane_ms_per_step": round(single / args.steps * 1e3, 4),
-                "single_lane_value": round(pixels / single / 1e6, 2),
-            },
+            "config": cfg,
             "roofline": {
+                # bound: the roofline the fraction is priced against (no MFMA work:
+                # HBM); what limits the kernels is `limiter`
                 "bound": "hbm",
-                "kernel": "k_front",
-                "achieved": round(achieved, 1),
+                "limiter": "issue/latency: wave-cycles parked at s_waitcnt/barrier and VALU+SALU issue "
+                           "(PMC parked_frac, valu_frac per kernel), not HBM bandwidth",
+                "kernel": dom,
+                "achieved": d.get("achieved"),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "avg_launch_us": round(avg_front_s * 1e6, 2),
-                "algorithmic_bytes_per_launch": algo_bytes,
-                "path": {"algorithmic_bytes_per_step": path_bytes, "achieved": round(path_achieved, 1),
+                "frac": d.get("frac"),
+                "traffic": d.get("traffic"),
+                "avg_launch_us": d.get("avg_launch_us"),
+                "algorithmic_bytes_per_launch": round(algo_bytes),
+                "algorithmic_bytes_def": "SURVEY 8(d): 3 B/px RGB in + JPEG bytes out, per frame, x frames per launch",
+                "kernels": kern,
+                "path": {"algorithmic_bytes_per_step": round(algo_bytes), "achieved": round(path_achieved, 1),
                          "frac": round(path_achieved / HBM_PEAK_GBS, 4)},
-                "valu": valu,
+                "pmc_source": f"profiles/pmc_{args.config}.json" if pmc else None,
             },
             "cpu_baseline": cpu,
             "ppm_ingest": ingest,

@@ -168,11 +168,21 @@ __device__ __forceinline__ uint32_t extra_bits(int v, int cat) {
 // table, 2 category range, 4 output capacity) is word k, set to 1 by a plain
 // vector store -- every writer stores the same value, so concurrent writers need
 // no atomics (none cross PCIe), and the host reads the words after the stream's
-// work without a copy.
+// work without a copy.  The active lanes' bits are ORed over the wave first and
+// only its first active lane stores: a fully bad frame costs one store per kind
+// per wave, not per thread.
 __device__ __forceinline__ void raise_status(int* status, int bits) {
+    const unsigned long long act = __ballot(1);
+    const int leader = (int)__ffsll((long long)act) - 1;
+    int wb = 0;
 #pragma unroll
     for (int k = 0; k < 5; ++k)
-        if (bits & (1 << k)) reinterpret_cast<volatile int*>(status)[k] = 1;
+        if (__ballot((bits >> k) & 1)) wb |= 1 << k;
+    if (lane_id() == leader) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            if (wb & (1 << k)) reinterpret_cast<volatile int*>(status)[k] = 1;
+    }
 }
 
 }  // namespace dmmt

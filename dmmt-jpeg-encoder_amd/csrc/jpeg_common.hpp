@@ -25,9 +25,11 @@ static constexpr int kHistReps = 8;  // (measured: 16 and 4 replicas pipeline 1-
 #define DMMT_CHUNK_BLOCKS 256
 #endif
 static constexpr int kChunkBlocks = DMMT_CHUNK_BLOCKS;
-// Worst-case entropy-coded bits of one block: DC code 16 + 12 extra bits, 63 AC
-// tokens of code 16 + 12 extra bits (|coef| <= 2048 for 8-bit-range input).
-static constexpr int kMaxBlockBits = 28 * 64;
+// Worst-case entropy-coded bits of one block: 64 tokens (the DC, then at most 63
+// AC tokens -- a ZRL or the EOB stands for at least one zero) of code <= 16 +
+// extra bits <= 15.  Integer samples keep |coef| <= 2049 (category <= 12), but
+// Image<f32> dots and host blocks reach category 15 (categorize.rs:22-32).
+static constexpr int kMaxBlockBits = 31 * 64;
 // Staging words of one chunk's bit stream (worst case).
 static constexpr long long kChunkWordsCap = (long long)kChunkBlocks * kMaxBlockBits / 32;
 // Upper bound of the header the table kernel writes (SOI..SOS incl. DRI).

@@ -626,7 +626,12 @@ def gather_striped(part, n: int, off: int, total: int, root: int = 0, group=None
 
     if rank != root:
         if n:
-            dist.send(part[:n], dst=peer(root), group=group)
+            # complete before returning: the caller may rewrite `part` (the next
+            # stripe_encode) as soon as this returns, and with RCCL the send runs on
+            # its own stream -- wait for it there, then for that on the host
+            dist.isend(part[:n], dst=peer(root), group=group).wait()
+            if part.is_cuda:
+                torch.cuda.current_stream(part.device).synchronize()
         return None
     out = torch.empty(total, dtype=torch.uint8, device=part.device)
     out[off:off + n].copy_(part[:n])

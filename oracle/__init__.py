@@ -82,6 +82,10 @@ def lib():
         L.ref_encode.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
         L.ref_encode_mt.restype = i32
         L.ref_encode_mt.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), i32, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+        L.ref_forward_par.restype = i32
+        L.ref_forward_par.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), i32, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
+        L.ref_encode_par.restype = i32
+        L.ref_encode_par.argtypes = [vp, i32, i32, i32, ctypes.POINTER(RefOptions), i32, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_size_t)]
         L.ref_free.argtypes = [vp]
         _lib = L
     return _lib
@@ -112,16 +116,21 @@ def _as_u16_rgb(rgb) -> np.ndarray:
 
 
 def encode(rgb, maxval: int, preset: int, luma_q, chroma_q, bits_per_channel: int = 8, threads: int = 1,
-           restart_interval: int = 0) -> bytes:
+           restart_interval: int = 0, parallel: bool = False) -> bytes:
     """Whole reference encode path (JpegImageWriter::write_image, jpeg.rs:64-75).
-    restart_interval > 0: the DRI/RSTn extension (not in the reference)."""
+    restart_interval > 0: the DRI/RSTn extension (not in the reference).
+    threads > 1: the DCT on a thread pool as transformer.rs:126-148; with parallel=True
+    every front-half stage is split over the threads (same bytes, test speed)."""
     a = _as_u16_rgb(rgb)
     h, w, _ = a.shape
     opt = make_options(preset, luma_q, chroma_q, bits_per_channel, restart_interval)
     out = ctypes.c_void_p()
     n = ctypes.c_size_t()
     L = lib()
-    if threads > 1:
+    if parallel:
+        rc = L.ref_encode_par(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), max(1, int(threads)),
+                              ctypes.byref(out), ctypes.byref(n))
+    elif threads > 1:
         rc = L.ref_encode_mt(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), int(threads), ctypes.byref(out), ctypes.byref(n))
     else:
         rc = L.ref_encode(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), ctypes.byref(out), ctypes.byref(n))
@@ -132,15 +141,20 @@ def encode(rgb, maxval: int, preset: int, luma_q, chroma_q, bits_per_channel: in
     return data
 
 
-def forward(rgb, maxval: int, preset: int, luma_q, chroma_q) -> np.ndarray:
-    """Front half: quantised zigzag blocks in MCU emission order, shape (nblocks, 64) int16."""
+def forward(rgb, maxval: int, preset: int, luma_q, chroma_q, threads: int = 1) -> np.ndarray:
+    """Front half: quantised zigzag blocks in MCU emission order, shape (nblocks, 64) int16
+    (threads > 1: every stage split over threads, the same blocks)."""
     a = _as_u16_rgb(rgb)
     h, w, _ = a.shape
     opt = make_options(preset, luma_q, chroma_q)
     out = ctypes.c_void_p()
     n = ctypes.c_size_t()
     L = lib()
-    rc = L.ref_forward(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), ctypes.byref(out), ctypes.byref(n))
+    if threads > 1:
+        rc = L.ref_forward_par(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), int(threads), ctypes.byref(out),
+                               ctypes.byref(n))
+    else:
+        rc = L.ref_forward(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), ctypes.byref(out), ctypes.byref(n))
     if rc != 0:
         raise OracleError(rc, "ref_forward")
     buf = ctypes.string_at(out.value, n.value * 128)

@@ -701,6 +701,199 @@ static int ref_forward_impl(const uint16_t* rgb, int width, int height, int maxv
     return REF_OK;
 }
 
+/* ------------------------------------------------------------ parallel front half
+ * The same stages as ref_forward_impl with every one of them split over threads
+ * (rows of the colour conversion and of the subsampling, blocks of the DCT, MCUs of
+ * quantisation).  Each output element is computed by exactly the function above,
+ * so the result is identical to ref_forward; only the wall time differs.  It keeps
+ * the parity tests of the BASELINE configs at their full size (32768^2, 1.07 Gpx)
+ * within a few seconds of oracle time.  Not the CPU baseline (ref_encode_mt keeps
+ * the reference's structure: only the DCT on the pool, transformer.rs:126-148). */
+typedef struct {
+    void (*fn)(void* ctx, size_t lo, size_t hi);
+    void* ctx;
+    size_t lo, hi;
+} par_job;
+
+static void* par_run(void* a) {
+    par_job* j = (par_job*)a;
+    j->fn(j->ctx, j->lo, j->hi);
+    return NULL;
+}
+
+static void parallel_for(size_t n, int threads, void (*fn)(void*, size_t, size_t), void* ctx) {
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > n) threads = n ? (int)n : 1;
+    par_job jobs[256];
+    pthread_t th[256];
+    if (threads > 256) threads = 256;
+    for (int t = 0; t < threads; ++t) {
+        jobs[t].fn = fn;
+        jobs[t].ctx = ctx;
+        jobs[t].lo = n * (size_t)t / (size_t)threads;
+        jobs[t].hi = n * (size_t)(t + 1) / (size_t)threads;
+    }
+    for (int t = 1; t < threads; ++t) pthread_create(&th[t], NULL, par_run, &jobs[t]);
+    par_run(&jobs[0]);
+    for (int t = 1; t < threads; ++t) pthread_join(th[t], NULL);
+}
+
+typedef struct {
+    const uint16_t* rgb;
+    int width, height, wp, maxval;
+    float *py, *pcb, *pcr;
+    volatile int bad;
+} par_color;
+
+static void par_color_rows(void* c_, size_t lo, size_t hi) {
+    par_color* c = (par_color*)c_;
+    for (size_t y = lo; y < hi; ++y) {
+        for (int x = 0; x < c->wp; ++x) {
+            float r = 0.0f, g = 0.0f, b = 0.0f;
+            if (x < c->width && (int)y < c->height) {
+                const uint16_t* px = c->rgb + (y * (size_t)c->width + (size_t)x) * 3;
+                if (px[0] > c->maxval || px[1] > c->maxval || px[2] > c->maxval) {
+                    c->bad = 1;
+                    return;
+                }
+                r = ref_normalize(px[0], (uint16_t)c->maxval);
+                g = ref_normalize(px[1], (uint16_t)c->maxval);
+                b = ref_normalize(px[2], (uint16_t)c->maxval);
+            }
+            float ycc[3];
+            ref_rgb_to_ycbcr(r, g, b, ycc);
+            size_t i = y * (size_t)c->wp + (size_t)x;
+            c->py[i] = ycc[0];
+            c->pcb[i] = ycc[1];
+            c->pcr[i] = ycc[2];
+        }
+    }
+}
+
+/* the subsampling of plane rows in whole 8-row block rows: ref_subsample_resort of
+ * a horizontal slab writes exactly the slab's part of the block-contiguous output */
+typedef struct {
+    const float* plane[3];
+    float* out[3];
+    int wp, hp, hr, vr, average;
+} par_sub;
+
+static void par_sub_rows(void* c_, size_t lo, size_t hi) {
+    par_sub* c = (par_sub*)c_;
+    for (size_t u = lo; u < hi; ++u) {  /* unit = (plane, block row of its output) */
+        int p = (int)(u % 3);
+        size_t br = u / 3;
+        int hr = p ? c->hr : 1, vr = p ? c->vr : 1;
+        int sw = c->wp / hr, sh = c->hp / vr;
+        if ((int)br * 8 >= sh) continue;
+        /* output rows [8 br, 8 br + 8) read plane rows [8 br vr, 8 (br + 1) vr) */
+        const float* slab = c->plane[p] + (size_t)br * 8 * (size_t)vr * (size_t)c->wp;
+        ref_subsample_resort(slab, c->wp, 8 * vr, hr, vr, p ? c->average : 0, 8,
+                             c->out[p] + (size_t)br * 8 * (size_t)sw);
+    }
+}
+
+typedef struct {
+    float* blocks;
+} par_dct;
+
+static void par_dct_blocks(void* c_, size_t lo, size_t hi) {
+    par_dct* c = (par_dct*)c_;
+    for (size_t i = lo; i < hi; ++i) ref_dct_block(c->blocks + i * 64);
+}
+
+typedef struct {
+    const float *by, *bcb, *bcr;
+    const ref_options* opt;
+    size_t line, cbx;
+    int n_luma;
+    int16_t* out;
+} par_quant;
+
+static void par_quant_mcus(void* c_, size_t lo, size_t hi) {
+    par_quant* c = (par_quant*)c_;
+    const int bpm = c->n_luma + 2;
+    for (size_t m = lo; m < hi; ++m) {
+        size_t mx = m % c->cbx, my = m / c->cbx;
+        size_t src[4];
+        int ns = 0;
+        if (c->opt->preset == REF_P444) {
+            src[ns++] = m;
+        } else if (c->opt->preset == REF_P422) {
+            src[ns++] = my * c->line + 2 * mx;
+            src[ns++] = my * c->line + 2 * mx + 1;
+        } else {
+            size_t r0 = 2 * my * c->line;
+            src[ns++] = r0 + 2 * mx;
+            src[ns++] = r0 + 2 * mx + 1;
+            src[ns++] = r0 + c->line + 2 * mx;
+            src[ns++] = r0 + c->line + 2 * mx + 1;
+        }
+        for (int s = 0; s < ns + 2; ++s) {
+            const float* blk = s < ns ? c->by + src[s] * 64 : (s == ns ? c->bcb : c->bcr) + m * 64;
+            const uint8_t* q = s < ns ? c->opt->luma_q : c->opt->chroma_q;
+            int16_t* o = c->out + (m * (size_t)bpm + (size_t)s) * 64;
+            for (int i = 0; i < 64; ++i) o[i] = ref_quantize_value(blk[ZIGZAG[i]], q[ZIGZAG[i]]);
+        }
+    }
+}
+
+int ref_forward_par(const uint16_t* rgb, int width, int height, int maxval, const ref_options* opt, int n_threads,
+                    int16_t** coef_zz, size_t* nblocks) {
+    int hr = opt->preset == REF_P444 ? 1 : 2, vr = opt->preset == REF_P420 ? 2 : 1;
+    if (width <= 0 || height <= 0) return REF_E_INVALID_ARGUMENT;
+    int wp = (width + 8 * hr - 1) / (8 * hr) * (8 * hr);
+    int hp = (height + 8 * vr - 1) / (8 * vr) * (8 * vr);
+    if (wp > 65535 || hp > 65535) return REF_E_INVALID_ARGUMENT;
+    size_t npx = (size_t)wp * hp;
+    float* planes = (float*)malloc(sizeof(float) * npx * 3);
+    if (!planes) return REF_E_OOM;
+    par_color pc = {rgb, width, height, wp, maxval, planes, planes + npx, planes + 2 * npx, 0};
+    parallel_for((size_t)hp, n_threads, par_color_rows, &pc);
+    if (pc.bad) {
+        free(planes);
+        return REF_E_VALUE_EXCEEDS_MAX;
+    }
+    size_t ny = npx, nc = npx / (size_t)(hr * vr);
+    float* by = (float*)malloc(sizeof(float) * (ny + 2 * nc));
+    if (!by) {
+        free(planes);
+        return REF_E_OOM;
+    }
+    par_sub ps = {{planes, planes + npx, planes + 2 * npx}, {by, by + ny, by + ny + nc}, wp, hp, hr, vr,
+                  opt->preset != REF_P444};
+    parallel_for((size_t)(hp / 8) * 3, n_threads, par_sub_rows, &ps);
+    free(planes);
+    par_dct pd = {by};
+    parallel_for((ny + 2 * nc) / 64, n_threads, par_dct_blocks, &pd);
+    int n_luma;
+    block_layout(opt->preset, &n_luma);
+    size_t nmcu = nc / 64;
+    size_t nb = nmcu * (size_t)(n_luma + 2);
+    int16_t* out = (int16_t*)malloc(sizeof(int16_t) * nb * 64);
+    if (!out) {
+        free(by);
+        return REF_E_OOM;
+    }
+    par_quant pq = {by, by + ny, by + ny + nc, opt, (size_t)wp / 8, (size_t)(wp / hr) / 8, n_luma, out};
+    parallel_for(nmcu, n_threads, par_quant_mcus, &pq);
+    free(by);
+    *coef_zz = out;
+    *nblocks = nb;
+    return REF_OK;
+}
+
+int ref_encode_par(const uint16_t* rgb, int width, int height, int maxval, const ref_options* opt, int n_threads,
+                   uint8_t** out, size_t* out_len) {
+    int16_t* coef = NULL;
+    size_t nb = 0;
+    int rc = ref_forward_par(rgb, width, height, maxval, opt, n_threads, &coef, &nb);
+    if (rc != REF_OK) return rc;
+    rc = ref_encode_coefficients(coef, nb, width, height, opt, out, out_len);
+    free(coef);
+    return rc;
+}
+
 int ref_forward(const uint16_t* rgb, int width, int height, int maxval, const ref_options* opt,
                 int16_t** coef_zz, size_t* nblocks) {
     return ref_forward_impl(rgb, width, height, maxval, opt, 1, coef_zz, nblocks);

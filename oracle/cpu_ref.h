@@ -80,6 +80,11 @@ int ref_encode(const uint16_t* rgb, int width, int height, int maxval, const ref
  * jobs, the reference's only parallel stage (transformer.rs:126-148). */
 int ref_encode_mt(const uint16_t* rgb, int width, int height, int maxval, const ref_options* opt,
                   int n_threads, uint8_t** out, size_t* out_len);
+/* the same results with every front-half stage split over n_threads (test speed only) */
+int ref_forward_par(const uint16_t* rgb, int width, int height, int maxval, const ref_options* opt, int n_threads,
+                    int16_t** coef_zz, size_t* nblocks);
+int ref_encode_par(const uint16_t* rgb, int width, int height, int maxval, const ref_options* opt, int n_threads,
+                   uint8_t** out, size_t* out_len);
 void ref_free(void* p);
 
 #ifdef __cplusplus

@@ -54,7 +54,9 @@ class StandInEncoder:
         self.mask = mask
 
     def profile(self):
-        return {"front": (0.05 * 3, 3)}
+        # summed ms and launches per stage (dmmt_ctx_profile): k_emit the longest
+        return {"front": (0.05 * 3, 3), "hist": (0.02 * 3, 3), "tables": (0.01 * 3, 3), "emit": (0.06 * 3, 3),
+                "offsets": (0.005 * 3, 3), "stuffwrite": (0.007 * 3, 3)}
 
     def d2h(self, d, n):
         return np.full(n // 4, 1000, np.uint32).tobytes()
@@ -93,9 +95,9 @@ def test_bench_two_ranks_gloo(tmp_path):
     # distinct synthetic frames per rank (no two ranks encode the same frames)
     f0 = {tuple(x[2:]) for x in r0["log"] if x[0] == "frames"}
     f1 = {tuple(x[2:]) for x in r1["log"] if x[0] == "frames"}
-    # the timed steps run pipelined over the default lanes, then once serially
-    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 1]
-    assert line["config"]["lanes"] == 4 and line["config"]["single_lane_ms_per_step"] > 0
+    # the timed steps run pipelined over the default lanes, then again with events (roofline)
+    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 4]
+    assert line["config"]["lanes"] == 4 and "single_lane_ms_per_step" not in line["config"]
     assert f0 and f1 and not (f0 & f1)
     # elapsed is the MAX over ranks: at least the slow rank's sleeps
     assert line["ms_per_step"] >= STEP_SLEEP[1] * 1e3 * 0.9
@@ -107,24 +109,59 @@ def test_bench_two_ranks_gloo(tmp_path):
 
 
 def test_bench_line_fields_single_rank(monkeypatch):
-    """N = 1, the BASELINE config (4K 4:4:4 q90): the roofline block carries the
-    HBM view of k_front and, from the committed PMC counters, its VALU view."""
+    """N = 1, the BASELINE config (4K 4:4:4 q90): the roofline block names the
+    longest kernel of the events pass, prices every kernel's launch against the
+    SURVEY 8(d) bytes of the frame, and carries the committed PMC counters."""
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
         monkeypatch.delenv(k, raising=False)
     import bench
     log, lines = [], []
-    bench.main(["--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0"],
+    bench.main(["--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0", "--latency"],
                make_encoder=lambda lr: StandInEncoder(lr, 0, log), emit=lines.append)
     line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["metric"] == "Mpixel/s encoded (4K PPM, q=90)"
+    cfg = line["config"]
+    assert cfg["input_slots"] == 12 and cfg["input_slots"] * 3840 * 2160 * 3 > 256 * 2**20  # past the MALL
+    assert cfg["single_lane_ms_per_step"] > 0
     rf = line["roofline"]
-    assert rf["kernel"] == "k_front" and rf["peak"] == 8000.0 and rf["unit"] == "GB/s"
-    assert rf["algorithmic_bytes_per_launch"] == 3840 * 2160 * 3
-    assert rf["avg_launch_us"] == pytest.approx(50.0)  # the stand-in's profile(): 0.15 ms over 3 launches
-    assert rf["frac"] == pytest.approx(rf["achieved"] / 8000.0, rel=1e-2)
+    assert rf["kernel"] == "k_emit" and rf["bound"] == "hbm" and rf["peak"] == 8000.0 and rf["unit"] == "GB/s"
+    algo = 3840 * 2160 * 3 + 1000  # RGB in + the stand-in's JPEG bytes
+    assert rf["algorithmic_bytes_per_launch"] == algo
+    assert rf["avg_launch_us"] == pytest.approx(60.0)
+    assert rf["frac"] == pytest.approx(algo / 60e-6 / 1e9 / 8000.0, rel=1e-3)
+    assert set(rf["kernels"]) == {"k_front", "k_hist", "k_tables", "k_emit", "k_offsets", "k_stuffwrite"}
+    for name, k in rf["kernels"].items():
+        assert k["frac"] == pytest.approx(algo / (k["avg_launch_us"] * 1e-6) / 1e9 / 8000.0, rel=1e-2)
     pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_4k444q90.json")))
-    assert rf["traffic"] == pmc["front_hbm_bytes_per_launch"]
-    v = rf["valu"]
-    assert v["wave_instructions_per_launch"] == round(pmc["kernels"]["k_front"]["SQ_INSTS_VALU"])
-    assert v["frac"] == pytest.approx(v["wave_instructions_per_launch"] / 50e-6 / bench.VALU_PEAK_PER_S, rel=1e-3)
+    assert rf["traffic"] == round(pmc["kernels"]["k_emit"]["hbm_bytes"])
+    assert rf["kernels"]["k_front"]["valu_wave_insts"] == round(pmc["kernels"]["k_front"]["SQ_INSTS_VALU"])
     assert line["cpu_baseline"] is None and line["ppm_ingest"] is None
+
+
+def make_standin(local_rank):
+    """picklable encoder factory for the spawned ranks"""
+    return StandInEncoder(local_rank, local_rank, [])
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_flag_spawns_ranks(monkeypatch):
+    """`bench.py --gpus 2` without a launcher (no WORLD_SIZE) starts the two rank
+    processes itself and reports n_gpus 2."""
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    import bench
+    lines = []
+    bench.main(["--gpus", "2", "--steps", "10", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0",
+                "--config", "1080p420q75x256"], make_encoder=make_standin, emit=lines.append)
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "independent frames x2"
+    assert line["ms_per_step"] >= STEP_SLEEP[1] * 1e3 * 0.9  # the MAX over ranks
+
+
+def test_bench_refuses_world_mismatch(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    import bench
+    with pytest.raises(SystemExit):
+        bench.main(["--gpus", "4", "--steps", "1", "--warmup", "0", "--cpu-seconds", "0", "--ppm-steps", "0"],
+                   make_encoder=lambda lr: StandInEncoder(lr, 0, []), emit=lambda l: None)
