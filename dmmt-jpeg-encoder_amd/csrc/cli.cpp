@@ -1,11 +1,14 @@
 // cli.cpp -- command line mirroring the reference's clap CLI (cli.rs:23-126,
 // main.rs:5-12): dmmt-jpeg-encoder <input_file> <output_file> [-b 8|16|32]
-// [-p P444|P422|P420] [-t N] [-q PRESET]; extensions: --quality Q, --device D.
+// [-p P444|P422|P420] [-t N] [-q PRESET]; extensions: --quality Q, --device D,
+// --gpus N / --devices A,B,.. (the image as MCU-row stripes over several GPUs),
+// --restart-interval N (DRI/RSTn every N MCUs).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/dmmt_jpeg.h"
 
@@ -29,7 +32,10 @@ static void usage() {
             "  -t, --threads <THREADS>                  accepted for compatibility (GPU encoder)\n"
             "  -q, --quantization_table <TABLE>         preset name or alias [default: Specification]\n"
             "      --quality <Q>                        IJG-scaled Annex K tables (extension)\n"
-            "      --device <D>                         GPU ordinal [default: 0]\n");
+            "      --device <D>                         GPU ordinal [default: 0]\n"
+            "      --gpus <N>                           encode as MCU-row stripes on GPUs 0..N-1 (extension)\n"
+            "      --devices <A,B,..>                   encode as MCU-row stripes on these GPUs (repeats allowed)\n"
+            "      --restart-interval <N>               DRI/RSTn every N MCUs [default: 0 = none] (extension)\n");
 }
 
 int main(int argc, char** argv) {
@@ -38,6 +44,7 @@ int main(int argc, char** argv) {
     const char* in = nullptr;
     const char* out = nullptr;
     int device = 0;
+    std::vector<int> devices;  // several GPUs: a multi-GPU context
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
         auto value = [&](const char* name) -> std::string {
@@ -83,6 +90,30 @@ int main(int argc, char** argv) {
             }
         } else if (a == "--device") {
             device = atoi(value("--device").c_str());
+        } else if (a == "--gpus") {
+            const int n = atoi(value("--gpus").c_str());
+            if (n < 1 || n > DMMT_MAX_GROUP) {
+                fprintf(stderr, "error: --gpus must be 1..%d\n", DMMT_MAX_GROUP);
+                return 2;
+            }
+            devices.clear();
+            for (int d = 0; d < n; ++d) devices.push_back(d);
+        } else if (a == "--devices") {
+            std::string v = value("--devices");
+            devices.clear();
+            for (size_t p = 0; p <= v.size();) {
+                size_t q = v.find(',', p);
+                if (q == std::string::npos) q = v.size();
+                const std::string t = v.substr(p, q - p);
+                if (t.empty() || t.find_first_not_of("0123456789") != std::string::npos) {
+                    fprintf(stderr, "error: invalid value '%s' for '--devices'\n", v.c_str());
+                    return 2;
+                }
+                devices.push_back(atoi(t.c_str()));
+                p = q + 1;
+            }
+        } else if (a == "--restart-interval") {
+            opt.restart_interval = atoi(value("--restart-interval").c_str());
         } else if (a == "-h" || a == "--help") {
             usage();
             return 0;
@@ -100,7 +131,8 @@ int main(int argc, char** argv) {
         return 2;
     }
     dmmt_ctx* ctx = nullptr;
-    int rc = dmmt_ctx_create(device, &ctx);
+    int rc = devices.size() > 1 ? dmmt_ctx_create_multi(devices.data(), (int)devices.size(), &ctx)
+                                : dmmt_ctx_create(devices.empty() ? device : devices[0], &ctx);
     if (rc == DMMT_OK) rc = dmmt_convert_ppm_to_jpeg(ctx, in, out, &opt);
     dmmt_ctx_destroy(ctx);
     if (rc != DMMT_OK) {  // main.rs:8-11

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/dmmt_jpeg.h"
+#include "group.hpp"
 #include "jpeg_common.hpp"
 #include "kernels.hpp"
 
@@ -70,6 +71,10 @@ struct Lane {
 };
 
 struct dmmt_ctx {
+    // a context of several GPUs (dmmt_ctx_create_multi): its member contexts and
+    // host threads (group.cpp); the single-device fields below are then unused and
+    // the single-device entry points act on member 0
+    dmmt::Group* group = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
@@ -462,6 +467,9 @@ int collect_async(dmmt_ctx* c, Lane* L, bool device_synced = false) {
 
 int set_device(dmmt_ctx* c) { return hip_err(hipSetDevice(c->device)); }
 
+// the context a single-device call acts on: a group's member 0, else itself
+dmmt_ctx* primary(dmmt_ctx* c) { return c && c->group ? group_member(c->group, 0) : c; }
+
 void destroy_lane(Lane* L, bool own_stream) {
     (void)hipStreamSynchronize(L->stream);
     if (L->status) (void)hipHostFree(L->status);
@@ -512,8 +520,38 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
     return DMMT_OK;
 }
 
+extern "C" int dmmt_ctx_create_multi(const int* device_ids, int n, dmmt_ctx** out) {
+    if (!out) return DMMT_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (!device_ids || n < 1 || n > DMMT_MAX_GROUP) return DMMT_E_INVALID_ARGUMENT;
+    dmmt::Group* g = nullptr;
+    const int rc = dmmt::group_create(device_ids, n, &g);
+    if (rc) return rc;
+    dmmt_ctx* c = new dmmt_ctx();
+    c->group = g;
+    c->device = device_ids[0];
+    *out = c;
+    return DMMT_OK;
+}
+
+extern "C" int dmmt_ctx_num_devices(const dmmt_ctx* c) {
+    if (!c) return 0;
+    return c->group ? dmmt::group_size(c->group) : 1;
+}
+
+extern "C" dmmt_ctx* dmmt_ctx_member(dmmt_ctx* c, int i) {
+    if (!c) return nullptr;
+    if (c->group) return dmmt::group_member(c->group, i);
+    return i == 0 ? c : nullptr;
+}
+
 extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     if (!c) return;
+    if (c->group) {
+        dmmt::group_destroy(c->group);
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     (void)sync_lanes(c);
     drain_events(c);
@@ -530,6 +568,7 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
 
 extern "C" int dmmt_ctx_set_lanes(dmmt_ctx* c, int n) {
     if (!c || n < 1 || n > DMMT_MAX_LANES) return DMMT_E_INVALID_ARGUMENT;
+    if (c->group) return dmmt::group_set_lanes(c->group, n);
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -555,6 +594,7 @@ extern "C" int dmmt_ctx_set_lanes(dmmt_ctx* c, int n) {
 
 extern "C" int dmmt_ctx_synchronize(dmmt_ctx* c) {
     if (!c) return DMMT_E_INVALID_ARGUMENT;
+    if (c->group) return dmmt::group_synchronize(c->group);
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -573,6 +613,7 @@ extern "C" size_t dmmt_max_jpeg_bytes(uint16_t width, uint16_t height, int32_t s
 }
 
 extern "C" int dmmt_encode_device(dmmt_ctx* c, const dmmt_device_frames* f, const dmmt_options* opt, void* stream) {
+    c = primary(c);
     if (!c || !f) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = validate(opt))) return rc;
@@ -653,6 +694,7 @@ extern "C" int dmmt_jpeg_encode_batch(dmmt_ctx* c, const dmmt_image* imgs, int n
         outs[i] = nullptr;
         lens[i] = 0;
     }
+    if (c->group) return dmmt::group_encode_batch(c->group, imgs, n, opt, outs, lens);  // frames round-robin
     std::lock_guard<std::mutex> lk(c->mu);
     if ((rc = set_device(c))) return rc;
     int i = 0;
@@ -677,11 +719,47 @@ extern "C" int dmmt_jpeg_encode_batch(dmmt_ctx* c, const dmmt_image* imgs, int n
 extern "C" int dmmt_jpeg_encode(dmmt_ctx* c, const dmmt_image* img, const dmmt_options* opt, uint8_t** out,
                                 size_t* out_len) {
     if (!out || !out_len) return DMMT_E_INVALID_ARGUMENT;
-    return dmmt_jpeg_encode_batch(c, img, 1, opt, out, out_len);
+    if (c && c->group && dmmt::group_size(c->group) > 1)  // one image over the group's GPUs
+        return dmmt_jpeg_encode_striped(c, img, opt, 0, out, out_len);
+    return dmmt_jpeg_encode_batch(primary(c), img, 1, opt, out, out_len);
+}
+
+extern "C" int dmmt_jpeg_encode_striped(dmmt_ctx* c, const dmmt_image* img, const dmmt_options* opt, int n_stripes,
+                                        uint8_t** out, size_t* out_len) {
+    if (!c || !out || !out_len) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = validate(opt)) || (rc = check_image(img))) return rc;
+    Geom g;
+    if ((rc = make_checked_geom(img->width, img->height, opt->subsampling, img->maxval, opt->restart_interval, &g)))
+        return rc;
+    *out = nullptr;
+    *out_len = 0;
+    if (!c->group) {  // one context: one stripe, the whole image
+        if (n_stripes > 1) return DMMT_E_INVALID_ARGUMENT;
+        return dmmt_jpeg_encode_batch(c, img, 1, opt, out, out_len);
+    }
+    return dmmt::group_encode_striped(c->group, img, opt, n_stripes, out, out_len);
+}
+
+extern "C" int dmmt_encode_device_multi(dmmt_ctx* c, const dmmt_device_frames* frames, int n,
+                                        const dmmt_options* opt) {
+    if (!c || !frames || n < 1 || n > dmmt_ctx_num_devices(c)) return DMMT_E_INVALID_ARGUMENT;
+    if (!c->group) return dmmt_encode_device(c, frames, opt, nullptr);
+    return dmmt::group_encode_device(c->group, frames, n, opt);
+}
+
+extern "C" int dmmt_encode_striped_device(dmmt_ctx* c, const dmmt_stripe* stripes, int n, const dmmt_options* opt,
+                                          uint8_t* const* d_outs, const size_t* caps, uint64_t* lens) {
+    if (!c || n < 1 || n > dmmt_ctx_num_devices(c)) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = validate(opt))) return rc;
+    if (!c->group) return dmmt::stripes_on_contexts(&c, nullptr, n, stripes, opt, d_outs, caps, lens);
+    return dmmt::group_encode_striped_device(c->group, stripes, n, opt, d_outs, caps, lens);
 }
 
 extern "C" int dmmt_forward_blocks(dmmt_ctx* c, const dmmt_image* img, const dmmt_options* opt, int16_t* coef,
                                    size_t cap_blocks, size_t* nblocks) {
+    c = primary(c);
     if (!c || !coef || !nblocks) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = validate(opt)) || (rc = check_image(img))) return rc;
@@ -711,6 +789,7 @@ extern "C" int dmmt_forward_blocks(dmmt_ctx* c, const dmmt_image* img, const dmm
 
 extern "C" int dmmt_encode_coefficients(dmmt_ctx* c, const int16_t* coef, size_t nblocks, uint16_t width,
                                         uint16_t height, const dmmt_options* opt, uint8_t** out, size_t* out_len) {
+    c = primary(c);
     if (!c || !coef || !out || !out_len) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = validate(opt))) return rc;
@@ -746,6 +825,7 @@ extern "C" int dmmt_encode_coefficients(dmmt_ctx* c, const int16_t* coef, size_t
 }
 
 extern "C" int dmmt_dct_transform(dmmt_ctx* c, float* blocks, size_t len) {
+    c = primary(c);
     if (!c || (!blocks && len) || len % 64) return DMMT_E_INVALID_ARGUMENT;
     if (len == 0) return DMMT_OK;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -798,11 +878,42 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
 
 extern "C" int dmmt_decode_ppm_device(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt_ppm_header* h,
                                       void* d_rgb, void* stream) {
+    c = primary(c);
     if (!c || !h || (!d_text && len) || (!d_rgb && h->width && h->height)) return DMMT_E_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
     if ((rc = set_device(c))) return rc;
     return decode_ppm(c, d_text, len, h, d_rgb, stream ? (hipStream_t)stream : c->stream);
+}
+
+// convert_ppm_to_jpeg over several GPUs: the samples parsed on the host
+// (dmmt_parse_ppm), the image encoded as MCU-row stripes, one per GPU
+static int convert_on_group(dmmt_ctx* c, const char* input_path, const char* output_path, const dmmt_options* opt) {
+    FILE* fi = fopen(input_path, "rb");
+    if (!fi) return DMMT_E_OPEN_INPUT;
+    FILE* fo = fopen(output_path, "wb");
+    if (!fo) {
+        fclose(fi);
+        return DMMT_E_OPEN_OUTPUT;
+    }
+    std::vector<uint8_t> data;
+    struct stat sst;
+    int rc = fstat(fileno(fi), &sst) == 0 ? DMMT_OK : DMMT_E_OPEN_INPUT;
+    if (!rc) {
+        data.resize((size_t)sst.st_size);
+        if ((data.empty() ? 0 : fread(data.data(), 1, data.size(), fi)) != data.size()) rc = DMMT_E_OPEN_INPUT;
+    }
+    fclose(fi);
+    dmmt_image img{};
+    uint8_t* jpg = nullptr;
+    size_t n = 0;
+    if (!rc) rc = dmmt_parse_ppm(data.data(), data.size(), &img);
+    if (!rc) rc = dmmt_jpeg_encode(c, &img, opt, &jpg, &n);
+    if (img.rgb) dmmt_free(const_cast<void*>(img.rgb));
+    if (rc == DMMT_OK && fwrite(jpg, 1, n, fo) != n) rc = DMMT_E_WRITE_IMAGE_DATA;
+    free(jpg);
+    if (fclose(fo) != 0 && rc == DMMT_OK) rc = DMMT_E_WRITE_END_OF_FILE;
+    return rc;
 }
 
 extern "C" int dmmt_convert_ppm_to_jpeg(dmmt_ctx* c, const char* input_path, const char* output_path,
@@ -813,6 +924,8 @@ extern "C" int dmmt_convert_ppm_to_jpeg(dmmt_ctx* c, const char* input_path, con
     if (!c || !input_path || !output_path) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = validate(opt))) return rc;
+    if (c->group && dmmt::group_size(c->group) > 1) return convert_on_group(c, input_path, output_path, opt);
+    c = primary(c);
     FILE* fi = fopen(input_path, "rb");  // open_input_file (lib.rs:43-47)
     if (!fi) return DMMT_E_OPEN_INPUT;
     FILE* fo = fopen(output_path, "wb");  // open_output_file (lib.rs:49-57)
@@ -931,6 +1044,7 @@ extern "C" const char* dmmt_strerror(int code) {
 
 extern "C" int dmmt_ctx_set_profiling(dmmt_ctx* c, int enable) {
     if (!c) return DMMT_E_INVALID_ARGUMENT;
+    if (c->group) return dmmt::group_set_profiling(c->group, enable);
     std::lock_guard<std::mutex> lk(c->mu);
     drain_events(c);
     c->profile = enable != 0;
@@ -944,6 +1058,7 @@ extern "C" int dmmt_ctx_set_profiling(dmmt_ctx* c, int enable) {
 
 extern "C" int dmmt_ctx_profile(dmmt_ctx* c, double* ms, int32_t* launches, int n_stages) {
     if (!c) return DMMT_E_INVALID_ARGUMENT;
+    if (c->group) return dmmt::group_profile(c->group, ms, launches, n_stages);
     std::lock_guard<std::mutex> lk(c->mu);
     (void)hipSetDevice(c->device);
     drain_events(c);
@@ -958,6 +1073,7 @@ extern "C" int dmmt_num_stages(void) { return ST_COUNT; }
 extern "C" const char* dmmt_stage_name(int s) { return s >= 0 && s < ST_COUNT ? kStageNames[s] : ""; }
 
 extern "C" int dmmt_device_malloc(dmmt_ctx* c, size_t bytes, void** ptr) {
+    c = primary(c);
     if (!c || !ptr) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -966,6 +1082,7 @@ extern "C" int dmmt_device_malloc(dmmt_ctx* c, size_t bytes, void** ptr) {
 }
 
 extern "C" int dmmt_device_free(dmmt_ctx* c, void* ptr) {
+    c = primary(c);
     if (!c) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -974,6 +1091,7 @@ extern "C" int dmmt_device_free(dmmt_ctx* c, void* ptr) {
 }
 
 extern "C" int dmmt_memcpy_h2d(dmmt_ctx* c, void* dst, const void* src, size_t bytes) {
+    c = primary(c);
     if (!c) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -982,6 +1100,7 @@ extern "C" int dmmt_memcpy_h2d(dmmt_ctx* c, void* dst, const void* src, size_t b
 }
 
 extern "C" int dmmt_memcpy_d2h(dmmt_ctx* c, void* dst, const void* src, size_t bytes) {
+    c = primary(c);
     if (!c) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -991,6 +1110,7 @@ extern "C" int dmmt_memcpy_d2h(dmmt_ctx* c, void* dst, const void* src, size_t b
 
 extern "C" int dmmt_fill_synthetic(dmmt_ctx* c, void* d_rgb, uint16_t width, uint16_t height, int32_t n_frames,
                                    int32_t first_frame, uint32_t seed) {
+    c = primary(c);
     if (!c || !d_rgb || n_frames <= 0) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -1001,6 +1121,7 @@ extern "C" int dmmt_fill_synthetic(dmmt_ctx* c, void* d_rgb, uint16_t width, uin
 
 extern "C" int dmmt_fill_synthetic_rows(dmmt_ctx* c, void* d_rgb, uint16_t width, uint16_t height, int32_t row0,
                                         int32_t rows, int32_t frame, uint32_t seed) {
+    c = primary(c);
     if (!c || !d_rgb || row0 < 0 || rows <= 0 || row0 + rows > height) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     if ((rc = set_device(c))) return rc;
@@ -1048,6 +1169,7 @@ extern "C" size_t dmmt_stripe_max_bytes(const dmmt_stripe* st, const dmmt_option
 
 extern "C" int dmmt_stripe_analyze(dmmt_ctx* c, const dmmt_stripe* st, const dmmt_options* opt,
                                    uint64_t hist[DMMT_STRIPE_HIST_WORDS]) {
+    c = primary(c);
     if (!c || !hist) return DMMT_E_INVALID_ARGUMENT;
     int rc;
     Geom g;
@@ -1138,6 +1260,7 @@ static int dc_category(int v) {
 }
 
 extern "C" int dmmt_stripe_dc_edges(dmmt_ctx* c, int16_t first_dc[3], int16_t last_dc[3]) {
+    c = primary(c);
     if (!c || !first_dc || !last_dc) return DMMT_E_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->stripe_pending || c->stripe_g.restart_interval != 0) return DMMT_E_INVALID_ARGUMENT;
@@ -1164,6 +1287,7 @@ extern "C" void dmmt_stripe_fix_dc_hist(uint64_t hist[DMMT_STRIPE_HIST_WORDS], c
 extern "C" int dmmt_stripe_measure(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS],
                                    const int16_t prev_last_dc[3], uint8_t* d_out, size_t out_cap, uint64_t* bits,
                                    uint32_t* first16) {
+    c = primary(c);
     if (!c || !hist_sum || !prev_last_dc || !d_out || !bits || !first16) return DMMT_E_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->stripe_pending || c->stripe_g.restart_interval != 0) return DMMT_E_INVALID_ARGUMENT;
@@ -1216,6 +1340,7 @@ extern "C" int dmmt_stripe_measure(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STR
 
 extern "C" int dmmt_stripe_write(dmmt_ctx* c, uint64_t bit_offset, uint32_t next_bits, uint32_t next16,
                                  uint64_t* out_len) {
+    c = primary(c);
     if (!c || !out_len || next_bits > 16) return DMMT_E_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->stripe_pending || !c->stripe_measured) return DMMT_E_INVALID_ARGUMENT;  // dmmt_stripe_measure first
@@ -1250,6 +1375,7 @@ extern "C" int dmmt_stripe_write(dmmt_ctx* c, uint64_t bit_offset, uint32_t next
 
 extern "C" int dmmt_stripe_encode(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRIPE_HIST_WORDS], uint8_t* d_out,
                                   size_t out_cap, uint64_t* out_len) {
+    c = primary(c);
     if (!c || !hist_sum || !d_out || !out_len) return DMMT_E_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!c->stripe_pending) return DMMT_E_INVALID_ARGUMENT;  // dmmt_stripe_analyze first

@@ -120,6 +120,14 @@ def lib():
     L.dmmt_stripe_fix_dc_hist.restype = None
     L.dmmt_stripe_measure.argtypes = [vp, H, I3, vp, sz, P(ctypes.c_uint64), P(ctypes.c_uint32)]
     L.dmmt_stripe_write.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_uint64)]
+    L.dmmt_ctx_create_multi.argtypes = [P(ctypes.c_int), ctypes.c_int, P(vp)]
+    L.dmmt_ctx_num_devices.argtypes = [vp]
+    L.dmmt_ctx_member.argtypes = [vp, ctypes.c_int]
+    L.dmmt_ctx_member.restype = vp
+    L.dmmt_jpeg_encode_striped.argtypes = [vp, P(DmmtImage), P(DmmtOptions), ctypes.c_int, P(vp), P(sz)]
+    L.dmmt_encode_device_multi.argtypes = [vp, P(DmmtDeviceFrames), ctypes.c_int, P(DmmtOptions)]
+    L.dmmt_encode_striped_device.argtypes = [vp, P(DmmtStripe), ctypes.c_int, P(DmmtOptions), P(vp), P(sz),
+                                             P(ctypes.c_uint64)]
     L.dmmt_build_info.argtypes = []
     L.dmmt_build_info.restype = ctypes.c_char_p
     _lib = L
@@ -316,12 +324,56 @@ def parse_ppm_header(data: bytes) -> DmmtPpmHeader:
 
 class Encoder:
     """A GPU context (dmmt_ctx): one device, one stream, pooled workspace.
-    Plays the role of the ThreadPool the reference passes around (lib.rs:62)."""
+    Plays the role of the ThreadPool the reference passes around (lib.rs:62).
+    ``devices=[...]``: a multi-GPU context (dmmt_ctx_create_multi), one member
+    context and host thread per id; encode() then splits the image into MCU-row
+    stripes over the members and encode_batch() deals frames round-robin."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None):
         self._ctx = ctypes.c_void_p()
-        _check(lib().dmmt_ctx_create(int(device), ctypes.byref(self._ctx)), f"dmmt_ctx_create({device})")
-        self.device = device
+        if devices is not None:
+            ids = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            _check(lib().dmmt_ctx_create_multi(ids, len(devices), ctypes.byref(self._ctx)),
+                   f"dmmt_ctx_create_multi({list(devices)})")
+            self.device = int(devices[0]) if len(devices) else 0
+        else:
+            _check(lib().dmmt_ctx_create(int(device), ctypes.byref(self._ctx)), f"dmmt_ctx_create({device})")
+            self.device = device
+
+    def num_devices(self) -> int:
+        return lib().dmmt_ctx_num_devices(self._ctx)
+
+    def member(self, i: int) -> int:
+        """member context i's handle (borrowed: valid while this context lives)"""
+        return lib().dmmt_ctx_member(self._ctx, int(i)) or 0
+
+    def encode_striped(self, image: "Image", options: "JpegTransformationOptions", n_stripes: int = 0) -> bytes:
+        """one image as MCU-row stripes over the members (dmmt_jpeg_encode_striped)"""
+        im = image.to_c()
+        out = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        _check(lib().dmmt_jpeg_encode_striped(self._ctx, ctypes.byref(im), ctypes.byref(options.to_c()),
+                                              int(n_stripes), ctypes.byref(out), ctypes.byref(n)), "encode_striped")
+        data = ctypes.string_at(out.value, n.value)
+        lib().dmmt_free(out)
+        return data
+
+    def encode_device_multi(self, frames, options: "JpegTransformationOptions"):
+        """frames[i]: a DmmtDeviceFrames in member i's HBM; enqueued, see synchronize()"""
+        arr = (DmmtDeviceFrames * len(frames))(*frames)
+        _check(lib().dmmt_encode_device_multi(self._ctx, arr, len(frames), ctypes.byref(options.to_c())),
+               "encode_device_multi")
+
+    def encode_striped_device(self, stripes, options: "JpegTransformationOptions", d_outs, caps):
+        """stripes[i] in member i's HBM; returns the byte count written to each d_outs[i]"""
+        n = len(stripes)
+        st = (DmmtStripe * n)(*stripes)
+        outs = (ctypes.c_void_p * n)(*d_outs)
+        cp = (ctypes.c_size_t * n)(*caps)
+        lens = (ctypes.c_uint64 * n)()
+        _check(lib().dmmt_encode_striped_device(self._ctx, st, n, ctypes.byref(options.to_c()), outs, cp, lens),
+               "encode_striped_device")
+        return [int(x) for x in lens]
 
     @property
     def handle(self):

@@ -205,6 +205,36 @@ int dmmt_stripe_measure(dmmt_ctx* ctx, const uint64_t hist_sum[DMMT_STRIPE_HIST_
 /* bit_offset: B_k; next16: the next_bits (<= 16) scan bits after the stripe, MSB-aligned */
 int dmmt_stripe_write(dmmt_ctx* ctx, uint64_t bit_offset, uint32_t next_bits, uint32_t next16, uint64_t* out_len);
 
+/* ---- several GPUs from one process (extension) ---------------------------------------------
+ * The reference's only fan-out is a CPU thread pool: ThreadPool::new(n) (lib.rs:62) handed to
+ * transform_on_threadpool (cosine_transform.rs:55-73) for the DCT.  A multi-GPU context is the
+ * GPU counterpart: one member context per device id (ids may repeat: several contexts on one
+ * GPU) and one host thread per member.  Every entry point accepts it:
+ *   dmmt_jpeg_encode / dmmt_convert_ppm_to_jpeg   the image as MCU-row stripes, one per member,
+ *                       the exchange of SURVEY.md 8(e) done on the host (no RCCL); the bytes
+ *                       are identical to a single-GPU encode (restart_interval 0: the
+ *                       reference's own stream, stripes joined mid-byte; > 0: stripes of whole
+ *                       restart intervals)
+ *   dmmt_jpeg_encode_batch   frames round-robin over the members, outputs in input order
+ *   dmmt_ctx_synchronize / _set_lanes / _set_profiling / _profile   every member
+ *   any other call (device memory, stage-level, stripe_* steps)      member 0
+ * Device-resident work names the member explicitly (dmmt_encode_device_multi,
+ * dmmt_encode_striped_device) or goes to a member context (dmmt_ctx_member). */
+#define DMMT_MAX_GROUP 64
+int dmmt_ctx_create_multi(const int* device_ids, int n, dmmt_ctx** out);
+int dmmt_ctx_num_devices(const dmmt_ctx* ctx);       /* members (1 for dmmt_ctx_create contexts) */
+dmmt_ctx* dmmt_ctx_member(dmmt_ctx* ctx, int i);     /* borrowed; a single-device context is its own member 0 */
+/* one host image as MCU-row stripes over the members (n_stripes <= 0: all of them; at most one
+ * per member; fewer where the image has fewer MCU rows or restart intervals) */
+int dmmt_jpeg_encode_striped(dmmt_ctx* ctx, const dmmt_image* img, const dmmt_options* opt, int n_stripes,
+                             uint8_t** out, size_t* out_len);
+/* frames[i] in member i's HBM (n_frames 0: none), enqueued as dmmt_encode_device with a NULL stream */
+int dmmt_encode_device_multi(dmmt_ctx* ctx, const dmmt_device_frames* frames, int n, const dmmt_options* opt);
+/* stripes[i] in member i's HBM, in row order from MCU row 0; stripe i's bytes to d_outs[i]
+ * (caps[i] >= dmmt_stripe_max_bytes), lens[i] = their count: concatenated, the JPEG file */
+int dmmt_encode_striped_device(dmmt_ctx* ctx, const dmmt_stripe* stripes, int n, const dmmt_options* opt,
+                               uint8_t* const* d_outs, const size_t* caps, uint64_t* lens);
+
 /* ---- stage-level entry points (parity tests) ---------------------------------------- */
 /* Front half only (transformer.rs:188-199): quantised zigzag blocks, MCU emission order
  * (block_fold_iterator.rs:53-148), 64 int16 per block, into coef (host). */

@@ -188,3 +188,20 @@ def test_ppm_header_errors(L):
         with pytest.raises(dmmt_jpeg.Error) as e:
             dmmt_jpeg.parse_ppm_header(text)
         assert e.value.code == code
+
+
+def test_multi_gpu_context_without_a_gpu(L):
+    """dmmt_ctx_create_multi: bad arguments are refused before any device is
+    touched; without a gfx950 GPU it fails like dmmt_ctx_create (no CPU fallback)"""
+    out = ctypes.c_void_p()
+    ids = (ctypes.c_int * 2)(0, 0)
+    assert L.dmmt_ctx_create_multi(ids, 0, ctypes.byref(out)) == -102
+    assert L.dmmt_ctx_create_multi(None, 2, ctypes.byref(out)) == -102
+    big = (ctypes.c_int * 65)()
+    assert L.dmmt_ctx_create_multi(big, 65, ctypes.byref(out)) == -102
+    rc = L.dmmt_ctx_create_multi(ids, 2, ctypes.byref(out))
+    if rc == 0:  # pragma: no cover - only on a GPU host
+        L.dmmt_ctx_destroy(out)
+    else:
+        assert rc == -202 and not out.value
+    assert L.dmmt_ctx_num_devices(None) == 0
