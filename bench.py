@@ -13,15 +13,16 @@ Prints ONE JSON line on rank 0.  `value` comes from the timed region: the
 production path, every call launched directly (six kernels per frame),
 consecutive frames pipelined over the context's lanes, the input frames rotating
 over enough distinct slots (> 256 MiB together) that their pixels stream from
-HBM rather than the 256 MiB Infinity Cache.  `roofline` comes from a second,
-identical pass with HIP events around every kernel launch, recorded on the
-stream the kernel runs on: per kernel the average launch duration, the
-SURVEY.md 8(d) algorithmic bytes over it, and the PMC traffic from profiles/;
-the dominant (longest) kernel is the headline.  Both passes run the same
-pipelined launches, so `rocprofv3 --kernel-trace --stats` of this command
-averages the same dispatches (profiles/r03_*).  `cpu_baseline` times the CPU
-restatement of the reference encoder (oracle/, C, the reference's DCT
-thread-pool structure) on a bounded sample of the same workload on this host.
+HBM rather than the 256 MiB Infinity Cache.  `roofline` comes from a second
+pass over the same steps, one frame at a time, with HIP events around every
+kernel launch, recorded on the stream the kernel runs on: per kernel the average
+launch duration, the SURVEY.md 8(d) algorithmic bytes over it, and the PMC
+traffic from profiles/; the dominant (longest) kernel is the headline.
+`rocprofv3 --kernel-trace` of this command times the same dispatches:
+scripts/kstats_passes.py splits its trace into the two passes (profiles/r03_*).
+`cpu_baseline` times the CPU restatement of the reference encoder (oracle/, C,
+the reference's DCT thread-pool structure) on a bounded sample of the same
+workload on this host.
 """
 import argparse
 import json
@@ -357,8 +358,6 @@ def main(argv=None, make_encoder=None, emit=None):
                     help="input slots the steps rotate over (0 = enough to exceed the 256 MiB Infinity Cache)")
     ap.add_argument("--mall-compare", action="store_true",
                     help="also time the steps over 4 input slots (inputs resident in the Infinity Cache)")
-    ap.add_argument("--latency", action="store_true",
-                    help="also time the steps one at a time (one lane): the latency of one frame")
     ap.add_argument("--ppm-steps", type=int, default=20,
                     help="PPM ingest line: P3 decodes of one synthetic frame timed on rank 0 (0 = skip)")
     ap.add_argument("--gather", action="store_true",
@@ -433,17 +432,17 @@ def main(argv=None, make_encoder=None, emit=None):
     # timed region: the production path (no event timing inside); with lanes > 1
     # consecutive frames are pipelined over the context's lanes (dmmt_ctx_set_lanes)
     elapsed = timed(lanes)
-    # roofline pass: the same pipelined steps again with HIP events around every
-    # kernel launch, on the stream it is launched on
+    # roofline pass: the same steps one at a time (one lane) with HIP events around
+    # every kernel launch, on the stream it is launched on: each kernel's own launch
+    # duration (pipelined, the kernels of consecutive frames share the CUs and each
+    # one's duration is stretched by the others)
     enc.set_profiling(1)
-    timed(lanes)
+    single = timed(1)
     prof = enc.profile()
     enc.set_profiling(0)
     extra = {}
     if args.mall_compare:  # inputs resident in the Infinity Cache: 4 slots
         extra["mall_resident_4_slots"] = timed(lanes, min(4, nslots))
-    if args.latency and lanes > 1:  # the same steps one at a time: the latency of one frame
-        extra["single_lane"] = timed(1)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -487,10 +486,9 @@ def main(argv=None, make_encoder=None, emit=None):
         if "mall_resident_4_slots" in extra:
             t4 = extra["mall_resident_4_slots"]
             cfg["mall_resident_4_slots_value"] = round(pixels / world / t4 / 1e6, 2)
-        if "single_lane" in extra:
-            t1 = extra["single_lane"]
-            cfg["single_lane_ms_per_step"] = round(t1 / args.steps * 1e3, 4)
-            cfg["single_lane_value"] = round(pixels / world / t1 / 1e6, 2)
+        # the roofline pass's wall time: one frame at a time, events on (the latency of
+        # a frame plus the event records)
+        cfg["single_lane_ms_per_step"] = round(single / args.steps * 1e3, 4)
         line = {
             "metric": "Mpixel/s encoded (4K PPM, q=90)" if args.config == "4k444q90" else f"Mpixel/s encoded ({args.config})",
             "value": round(value, 2),

@@ -116,6 +116,9 @@ __device__ __forceinline__ int coef_at(const BlockCoef& b, int k) {
 // MI355X -- the first block of a wave, nondeterministically; this form is exact
 // on the parity suite.)
 __device__ __forceinline__ void zigzag_in_registers(BlockCoef& b) {
+#ifdef DMMT_WALK_COLUMN_MAJOR
+    return;
+#endif
     uint32_t z[32];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
@@ -143,7 +146,11 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
 #pragma unroll
     for (int k = 1; k < 64; ++k) {
         if (k > kmax) continue;  // (wave-uniform) every later position is zero in every lane
+#ifdef DMMT_WALK_COLUMN_MAJOR  // study build: the walk straight over the column-major block
+        const int v = coef_at(b, coef_pos(k));
+#else
         const int v = coef_at(b, k);
+#endif
         if (v != 0) {
             const int r16 = 16 * k - l16;
             for (int r = r16 >> 8; r > 0; --r) sink(z & 0xFFFFu, (int)(z >> 16));

@@ -157,9 +157,10 @@ def forward(rgb, maxval: int, preset: int, luma_q, chroma_q, threads: int = 1) -
         rc = L.ref_forward(a.ctypes.data, w, h, int(maxval), ctypes.byref(opt), ctypes.byref(out), ctypes.byref(n))
     if rc != 0:
         raise OracleError(rc, "ref_forward")
-    buf = ctypes.string_at(out.value, n.value * 128)
+    # (a copy through numpy: ctypes.string_at takes an int size, < 2 GiB)
+    arr = np.ctypeslib.as_array((ctypes.c_int16 * (n.value * 64)).from_address(out.value)).reshape(n.value, 64).copy()
     L.ref_free(out)
-    return np.frombuffer(buf, dtype=np.int16).reshape(n.value, 64).copy()
+    return arr
 
 
 def encode_coefficients(coef_zz: np.ndarray, width: int, height: int, preset: int, luma_q, chroma_q,

@@ -95,9 +95,9 @@ def test_bench_two_ranks_gloo(tmp_path):
     # distinct synthetic frames per rank (no two ranks encode the same frames)
     f0 = {tuple(x[2:]) for x in r0["log"] if x[0] == "frames"}
     f1 = {tuple(x[2:]) for x in r1["log"] if x[0] == "frames"}
-    # the timed steps run pipelined over the default lanes, then again with events (roofline)
-    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 4]
-    assert line["config"]["lanes"] == 4 and "single_lane_ms_per_step" not in line["config"]
+    # the timed steps run pipelined over the default lanes, then one at a time with events (roofline)
+    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 1]
+    assert line["config"]["lanes"] == 4 and line["config"]["single_lane_ms_per_step"] > 0
     assert f0 and f1 and not (f0 & f1)
     # elapsed is the MAX over ranks: at least the slow rank's sleeps
     assert line["ms_per_step"] >= STEP_SLEEP[1] * 1e3 * 0.9
@@ -116,7 +116,7 @@ def test_bench_line_fields_single_rank(monkeypatch):
         monkeypatch.delenv(k, raising=False)
     import bench
     log, lines = [], []
-    bench.main(["--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0", "--latency"],
+    bench.main(["--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0"],
                make_encoder=lambda lr: StandInEncoder(lr, 0, log), emit=lines.append)
     line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["metric"] == "Mpixel/s encoded (4K PPM, q=90)"
