@@ -869,8 +869,8 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
     HIP_TRY(hipStreamSynchronize(st));
     const bool comments = (uint32_t)misc[2] != 0;
     const uint32_t s = comments ? (uint32_t)misc[0] : (uint32_t)(misc[0] >> 32);
-    if (s & 1u) return DMMT_E_PPM_PARSE_TOKEN;
-    if (misc[1] % 3) return DMMT_E_PPM_INCOMPLETE_PIXEL;
+    if (s & 1u) return dmmt::error_detail(DMMT_E_PPM_PARSE_TOKEN, 4);  // "Color Component Value"
+    if (misc[1] % 3) return dmmt::error_detail(DMMT_E_PPM_INCOMPLETE_PIXEL, (int)(misc[1] % 3));
     if (misc[1] != ns) return DMMT_E_PPM_SIZE_MISMATCH;
     if (s & 2u) return DMMT_E_VALUE_EXCEEDS_MAX;
     return DMMT_OK;

@@ -102,4 +102,8 @@ inline size_t max_jpeg_bytes(const Geom& g) {
     return (size_t)kMaxHeaderBytes + (size_t)g.max_scan_bytes * 2 + 4 * (size_t)g.nmcu + 2 + 64;
 }
 
+// host: record the payload of a reference error variant for dmmt_last_error_detail /
+// dmmt_last_error_message (ppm.cpp); returns code
+int error_detail(int code, int detail);
+
 }  // namespace dmmt

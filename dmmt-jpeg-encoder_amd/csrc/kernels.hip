@@ -312,6 +312,13 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     constexpr int NYB = 32 * VR;     // Y blocks: 32 columns x VR rows
     constexpr int CB = TM;           // chroma blocks per component
     constexpr int BS = 72;           // LDS floats per block: 64 + pad (conflict-free column reads)
+    // Block b starts at b * BS + 4 * f(b), f(b) = bit 2 of b, flipped for Cr: the
+    // 16-byte row stores of phase A (ds_write_b128, lanes in groups of 8 on 8
+    // consecutive blocks -- and Cb next to Cr with 4:2:x) start on 8 distinct
+    // 4-bank offsets mod 32, and the column reads of phase C (32 lanes = 4
+    // consecutive blocks x 8 columns) still hit 32 distinct banks.  With the plain
+    // stride the stores were 2-way conflicted.
+    auto blk_base = [](int b) { return b * BS + 4 * (((b >> 2) ^ (b >= NYB + CB ? 1 : 0)) & 1); };
     constexpr int SP = HR;           // threads per (chroma row, chroma block): one per luma block column
     constexpr int NJ = 8 * CB * SP;  // fused jobs (chroma row, chroma block, luma block column): 256
     constexpr int NCS = 8 / SP;      // chroma samples of a job
@@ -323,7 +330,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
     using Raw = RawTile<Sample, ROWS>;
 
     // row-transformed blocks (A -> C)
-    __shared__ __attribute__((aligned(16))) float sT[NB * BS];
+    __shared__ __attribute__((aligned(16))) float sT[NB * BS + 4];
     __shared__ __attribute__((aligned(16))) uint8_t sRaw[Raw::BYTES];
     __shared__ float sLut[256];
     __shared__ float sQ[128];
@@ -457,17 +464,17 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
             for (int dy = 0; dy < VR; ++dy) {
                 const int ly = r * VR + dy;
                 arai8(yv[dy]);
-                float4* o = reinterpret_cast<float4*>(sT + ((ly >> 3) * 32 + c * HR + h) * BS + (ly & 7) * 8);
+                float4* o = reinterpret_cast<float4*>(sT + blk_base((ly >> 3) * 32 + c * HR + h) + (ly & 7) * 8);
                 o[0] = make_float4(yv[dy][0], yv[dy][1], yv[dy][2], yv[dy][3]);
                 o[1] = make_float4(yv[dy][4], yv[dy][5], yv[dy][6], yv[dy][7]);
             }
             if constexpr (SP == 1) {
                 arai8(cbv);
                 arai8(crv);
-                float4* ob = reinterpret_cast<float4*>(sT + (NYB + c) * BS + r * 8);
+                float4* ob = reinterpret_cast<float4*>(sT + blk_base(NYB + c) + r * 8);
                 ob[0] = make_float4(cbv[0], cbv[1], cbv[2], cbv[3]);
                 ob[1] = make_float4(cbv[4], cbv[5], cbv[6], cbv[7]);
-                float4* orr = reinterpret_cast<float4*>(sT + (NYB + CB + c) * BS + r * 8);
+                float4* orr = reinterpret_cast<float4*>(sT + blk_base(NYB + CB + c) + r * 8);
                 orr[0] = make_float4(crv[0], crv[1], crv[2], crv[3]);
                 orr[1] = make_float4(crv[4], crv[5], crv[6], crv[7]);
             } else {
@@ -484,7 +491,7 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                     fr[4 + k] = h ? crv[k] : recv;
                 }
                 arai8(fr);
-                float4* oc = reinterpret_cast<float4*>(sT + (NYB + (h ? CB : 0) + c) * BS + r * 8);
+                float4* oc = reinterpret_cast<float4*>(sT + blk_base(NYB + (h ? CB : 0) + c) + r * 8);
                 oc[0] = make_float4(fr[0], fr[1], fr[2], fr[3]);
                 oc[1] = make_float4(fr[4], fr[5], fr[6], fr[7]);
             }
@@ -513,8 +520,9 @@ __global__ __launch_bounds__(256, WPE) void k_front(const Sample* __restrict__ r
                 const float* q = sQ + (blk < NYB ? 0 : 64) + col;
                 const float* rq = sRQ + (blk < NYB ? 0 : 64) + col;
                 float v[8];
+                const float* tb = sT + blk_base(blk) + col;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) v[i] = sT[blk * BS + i * 8 + col];
+                for (int i = 0; i < 8; ++i) v[i] = tb[i * 8];
                 if constexpr (SB == 4) {  // Image<f32> dots: unbounded coefficients
                     arai8(v);
                     quantize_col8(v, q, rq, x);

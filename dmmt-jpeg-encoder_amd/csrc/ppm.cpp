@@ -62,22 +62,63 @@ bool parse_u16(const std::string& t, uint16_t* out) {
 
 }  // namespace
 
+// The payload the reference's error::Error variants carry (error.rs:3-22), for the
+// last error a PPM entry point returned on this thread: IncompletePixelParsed(n)
+// carries n, the components of the unfinished pixel (ppm.rs:239-245);
+// PPMFileDoesNotContainRequiredToken and ParsingOfTokenFailed the token's name
+// (ppm.rs:80-84) -- here its index.
+static thread_local int t_err_code = 0, t_err_detail = 0;
+static const char* const kTokenNames[5] = {"P3 Header", "Width Header", "Height Header", "Max Value Header",
+                                           "Color Component Value"};
+enum { TOK_P3 = 0, TOK_WIDTH, TOK_HEIGHT, TOK_MAXVAL, TOK_COMPONENT };
+
+namespace dmmt {
+int error_detail(int code, int detail) {
+    t_err_code = code;
+    t_err_detail = detail;
+    return code;
+}
+}  // namespace dmmt
+using dmmt::error_detail;
+
+extern "C" int dmmt_last_error_detail(void) { return t_err_detail; }
+
+extern "C" const char* dmmt_last_error_message(void) {
+    // error.rs:25-60 Display of the variant, with its payload
+    static thread_local char msg[160];
+    switch (t_err_code) {
+    case DMMT_E_PPM_MISSING_TOKEN:
+        snprintf(msg, sizeof msg, "Expected token '%s' not found in PPM file", kTokenNames[t_err_detail % 5]);
+        break;
+    case DMMT_E_PPM_PARSE_TOKEN:
+        snprintf(msg, sizeof msg, "Parsing of token '%s' failed", kTokenNames[t_err_detail % 5]);
+        break;
+    case DMMT_E_PPM_INCOMPLETE_PIXEL:
+        snprintf(msg, sizeof msg, "Incomplete pixel parsed. Expected 3 components, but got %d.", t_err_detail);
+        break;
+    default:
+        snprintf(msg, sizeof msg, "%s", dmmt_strerror(t_err_code));
+    }
+    return msg;
+}
+
 // parse_header .. parse_max_value (ppm.rs:145-222): the four header tokens; the
 // body starts after the whitespace byte that ended the max value
 static int parse_header(Tokenizer& tz, dmmt_ppm_header* hdr) {
     std::string tok;
     memset(hdr, 0, sizeof *hdr);
     // parse_header + check_header_version (ppm.rs:177-192)
-    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
+    error_detail(DMMT_OK, 0);
+    if (!tz.next(tok)) return error_detail(DMMT_E_PPM_MISSING_TOKEN, TOK_P3);
     const bool binary = tok == "P6";
-    if (tok != "P3" && !binary) return DMMT_E_PPM_MISSING_TOKEN;
+    if (tok != "P3" && !binary) return error_detail(DMMT_E_PPM_MISSING_TOKEN, TOK_P3);
     uint16_t w, h, mx;
-    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
-    if (!parse_u16(tok, &w)) return DMMT_E_PPM_PARSE_TOKEN;
-    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
-    if (!parse_u16(tok, &h)) return DMMT_E_PPM_PARSE_TOKEN;
-    if (!tz.next(tok)) return DMMT_E_PPM_MISSING_TOKEN;
-    if (!parse_u16(tok, &mx)) return DMMT_E_PPM_PARSE_TOKEN;
+    if (!tz.next(tok)) return error_detail(DMMT_E_PPM_MISSING_TOKEN, TOK_WIDTH);
+    if (!parse_u16(tok, &w)) return error_detail(DMMT_E_PPM_PARSE_TOKEN, TOK_WIDTH);
+    if (!tz.next(tok)) return error_detail(DMMT_E_PPM_MISSING_TOKEN, TOK_HEIGHT);
+    if (!parse_u16(tok, &h)) return error_detail(DMMT_E_PPM_PARSE_TOKEN, TOK_HEIGHT);
+    if (!tz.next(tok)) return error_detail(DMMT_E_PPM_MISSING_TOKEN, TOK_MAXVAL);
+    if (!parse_u16(tok, &mx)) return error_detail(DMMT_E_PPM_PARSE_TOKEN, TOK_MAXVAL);
     hdr->width = w;
     hdr->height = h;
     hdr->maxval = mx;
@@ -132,7 +173,7 @@ extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) 
             uint16_t v;
             if (!parse_u16(tok, &v)) {
                 free(buf);
-                return DMMT_E_PPM_PARSE_TOKEN;
+                return error_detail(DMMT_E_PPM_PARSE_TOKEN, TOK_COMPONENT);
             }
             if (count < cap) {
                 if (sb == 1)
@@ -145,7 +186,7 @@ extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) 
         }
         if (count % 3) {  // check_pixel_was_complete (ppm.rs:239-245)
             free(buf);
-            return DMMT_E_PPM_INCOMPLETE_PIXEL;
+            return error_detail(DMMT_E_PPM_INCOMPLETE_PIXEL, (int)(count % 3));
         }
         if (count != npx * 3) {  // ppm.rs:165-175
             free(buf);

@@ -43,10 +43,18 @@ _lib = None
 class Error(Exception):
     """error::Error (src/error.rs:3-22) plus the states where the reference panics."""
 
+    PPM_CODES = (-1, -2, -3)  # the variants with a payload (error.rs:4-7)
+
     def __init__(self, code: int, context: str = ""):
         self.code = code
         self.name = lib().dmmt_error_name(code).decode() if _lib is not None else str(code)
         msg = lib().dmmt_strerror(code).decode() if _lib is not None else str(code)
+        # the variant's payload (read right after the failing call, same thread):
+        # IncompletePixelParsed(n) -> n; the token index of the two token errors
+        self.detail = lib().dmmt_last_error_detail() if _lib is not None and code in self.PPM_CODES else None
+        self.n = self.detail if code == -3 else None
+        if self.detail is not None:
+            msg = lib().dmmt_last_error_message().decode()
         super().__init__(f"{self.name}: {msg}" + (f" ({context})" if context else ""))
 
 
@@ -128,6 +136,9 @@ def lib():
     L.dmmt_encode_device_multi.argtypes = [vp, P(DmmtDeviceFrames), ctypes.c_int, P(DmmtOptions)]
     L.dmmt_encode_striped_device.argtypes = [vp, P(DmmtStripe), ctypes.c_int, P(DmmtOptions), P(vp), P(sz),
                                              P(ctypes.c_uint64)]
+    L.dmmt_last_error_detail.argtypes = []
+    L.dmmt_last_error_message.argtypes = []
+    L.dmmt_last_error_message.restype = ctypes.c_char_p
     L.dmmt_build_info.argtypes = []
     L.dmmt_build_info.restype = ctypes.c_char_p
     _lib = L

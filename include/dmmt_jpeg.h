@@ -280,6 +280,15 @@ int dmmt_decode_ppm_device(dmmt_ctx* ctx, const uint8_t* d_text, size_t len, con
  * them on the GPU (dmmt_decode_ppm_device, then the encode path), write the file. */
 int dmmt_convert_ppm_to_jpeg(dmmt_ctx* ctx, const char* input_path, const char* output_path,
                              const dmmt_options* opt);
+/* The payload the reference's Error variant carries (error.rs:3-22), for the last error a PPM
+ * entry point (dmmt_parse_ppm, dmmt_read_ppm, dmmt_parse_ppm_header, dmmt_decode_ppm_device,
+ * dmmt_convert_ppm_to_jpeg) returned on the calling thread: IncompletePixelParsed(n) -> n
+ * (ppm.rs:239-245); PPMFileDoesNotContainRequiredToken / ParsingOfTokenFailed -> the token
+ * (0 "P3 Header", 1 "Width Header", 2 "Height Header", 3 "Max Value Header", 4 "Color
+ * Component Value", ppm.rs:80-84).  dmmt_last_error_message: the variant's Display text with
+ * that payload (error.rs:25-60). */
+int dmmt_last_error_detail(void);
+const char* dmmt_last_error_message(void);
 void dmmt_free(void* p);
 const char* dmmt_strerror(int code);
 /* name of the error variant as in error.rs ("MismatchOfSizeBetweenHeaderAndValues", ...) */

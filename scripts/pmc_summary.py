@@ -9,7 +9,7 @@ from collections import defaultdict
 root = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 acc = defaultdict(lambda: defaultdict(list))
-for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(root, "**", "run_counter_collection.csv"), recursive=True)):
     per = defaultdict(float)
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]

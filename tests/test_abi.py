@@ -205,3 +205,42 @@ def test_multi_gpu_context_without_a_gpu(L):
     else:
         assert rc == -202 and not out.value
     assert L.dmmt_ctx_num_devices(None) == 0
+
+
+# ppm.rs:266-306, the reference's own PPM unit tests, as data
+PPM_KATS = [
+    ("read_string", "P3\n# Example PPM image string\n3 2\n255\n255 0 0   0 255 0   0 0 255\n255 255 0  255 0 255  0 255 255",
+     None),
+    ("read_continuous_string", "P3 3 2 255 255 0 0   0 255 0   0 0 255 255 255 0  255 0 255  0 255 255", None),
+    ("read_newline_string", "P3\n# Example PPM image newlines\n3\n2\n255\n255\n0\n0\n0\n255\n0\n0\n0\n255\n255\n255\n0\n"
+     "255\n0\n255\n0\n255\n255", None),
+    ("incomplete_pixel", "P3\n3 2 255 0 0 255 0 0", (-3, 2)),
+    ("wrong_size", "P3\n3 2 255 0 0 255", (-4, None)),
+]
+
+
+@pytest.mark.parametrize("name,text,err", PPM_KATS, ids=[k[0] for k in PPM_KATS])
+def test_reference_ppm_unit_tests(L, name, text, err):
+    """ppm.rs:266-306 through the host reader (PPMImageReader::read_image)"""
+    if err is None:
+        img = dmmt_jpeg.PPMImageReader(text.encode()).read_image()
+        assert img.height == 2 and img.width == 3
+        assert img.samples.reshape(-1).tolist()[:6] == [255, 0, 0, 0, 255, 0]
+        return
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        dmmt_jpeg.PPMImageReader(text.encode()).read_image()
+    assert e.value.code == err[0]
+    if err[1] is not None:  # IncompletePixelParsed(n), n == 2 (ppm.rs:290-293)
+        assert e.value.n == err[1]
+        assert "Expected 3 components, but got 2." in str(e.value)
+
+
+@pytest.mark.parametrize("text,code,token", [(b"", -1, "P3 Header"), (b"P5 1 1 255", -1, "P3 Header"),
+                                             (b"P3 1", -1, "Height Header"), (b"P3 x 1 255", -2, "Width Header"),
+                                             (b"P3 1 1 99999 0 0 0", -2, "Max Value Header"),
+                                             (b"P3 1 1 255 0 0 -1", -2, "Color Component Value")])
+def test_ppm_error_payload_token_names(L, text, code, token):
+    """error.rs:28-33: the token errors name the token (ppm.rs:80-84)"""
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        dmmt_jpeg.PPMImageReader(text).read_image()
+    assert e.value.code == code and f"'{token}'" in str(e.value)

@@ -202,3 +202,23 @@ def test_convert_decodes_on_the_gpu(tmp_path, spec_tables):
     with pytest.raises(dmmt_jpeg.Error) as e:
         dmmt_jpeg.convert_ppm_to_jpeg(dmmt_jpeg.Arguments(str(bad), str(out)))
     assert e.value.code == -2
+
+
+from test_abi import PPM_KATS  # noqa: E402  (ppm.rs:266-306 as data)
+
+
+@pytest.mark.parametrize("name,text,err", PPM_KATS, ids=[k[0] for k in PPM_KATS])
+def test_reference_ppm_unit_tests_on_gpu(encoder, name, text, err):
+    """the reference's five PPM unit tests (ppm.rs:266-306) with the body decoded on
+    the GPU (dmmt_decode_ppm_device); IncompletePixelParsed carries n == 2"""
+    data = text.encode()
+    if err is None:
+        img = encoder.read_ppm_device(data)
+        host = dmmt_jpeg.PPMImageReader(data).read_image()
+        assert img.height == 2 and np.array_equal(img.samples, host.samples)
+        return
+    with pytest.raises(dmmt_jpeg.Error) as e:
+        encoder.read_ppm_device(data)
+    assert e.value.code == err[0]
+    if err[1] is not None:
+        assert e.value.n == err[1]
