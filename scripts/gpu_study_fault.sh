@@ -8,6 +8,6 @@ set -o pipefail
 O=gpurun_out/fault
 mkdir -p $O
 ( cd study_wip && timeout -k 10 240 python scripts/debug_determinism.py --n 4 ) > $O/wip.log 2>&1; echo "wip rc=$?"; cat $O/wip.log | grep -v amdgpu.ids
-DMMT_LIB_PATH=$PWD/dmmt-jpeg-encoder_amd/lib_colmajor/libdmmt_jpeg.so timeout -k 10 240 python tests/tools/debug_determinism.py --n 4 > $O/colmajor.log 2>&1; echo "colmajor rc=$?"; grep -v amdgpu.ids $O/colmajor.log
-timeout -k 10 240 python tests/tools/debug_determinism.py --n 2 > $O/product.log 2>&1; echo "product rc=$?"; grep -v amdgpu.ids $O/product.log
+DMMT_LIB_PATH=$PWD/dmmt-jpeg-encoder_amd/lib_colmajor/libdmmt_jpeg.so timeout -k 10 240 python tests/tools/determinism.py --n 4 > $O/colmajor.log 2>&1; echo "colmajor rc=$?"; grep -v amdgpu.ids $O/colmajor.log
+timeout -k 10 240 python tests/tools/determinism.py --n 2 > $O/product.log 2>&1; echo "product rc=$?"; grep -v amdgpu.ids $O/product.log
 echo exit=0

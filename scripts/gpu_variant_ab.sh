@@ -21,7 +21,7 @@ for c in $CFGS; do
       if [ "$v" = base ]; then unset DMMT_LIB_PATH; else export DMMT_LIB_PATH=$VLIB; fi
       for s in 20 200; do
         timeout -k 10 200 python bench.py --config $c --steps $s --warmup 5 --cpu-seconds 0 --ppm-steps 0 > $O/b_${c}_${v}_${s}_$r.json 2>> $O/bench.err || { echo "bench $v failed"; exit 1; }
-        python -c "import json; d=json.load(open('$O/b_${c}_${v}_${s}_$r.json')); print('$c', '$v', 'steps $s', d['value'], 'single', d['config']['single_lane_value'])"
+        python -c "import json; d=json.load(open('$O/b_${c}_${v}_${s}_$r.json')); print('$c', '$v', 'steps $s', d['value'], 'single', d['config']['single_lane_ms_per_step'])"
       done
     done
   done
