@@ -853,7 +853,7 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
     if ((rc = ensure(c->ppm_misc, 64, true))) return rc;
     uint64_t misc[4] = {0, 0, 0, 0};  // PpmMisc: status | status_fast << 32, tokens, flag
     if (h->binary) {  // P6 (extension): raw big-endian samples after the header, as dmmt_parse_ppm
-        if (len - h->body_offset < ns * (unsigned long long)sb) return DMMT_E_PPM_SIZE_MISMATCH;
+        if (len - h->body_offset < ns * (unsigned long long)sb) return dmmt::error_detail(DMMT_E_PPM_SIZE_MISMATCH, 0);
         HIP_TRY(launch_ppm_p6(d_text + h->body_offset, d_rgb, sb, ns, h->maxval, nullptr, st));
         HIP_TRY(hipStreamSynchronize(st));
         return DMMT_OK;
@@ -871,7 +871,7 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
     const uint32_t s = comments ? (uint32_t)misc[0] : (uint32_t)(misc[0] >> 32);
     if (s & 1u) return dmmt::error_detail(DMMT_E_PPM_PARSE_TOKEN, 4);  // "Color Component Value"
     if (misc[1] % 3) return dmmt::error_detail(DMMT_E_PPM_INCOMPLETE_PIXEL, (int)(misc[1] % 3));
-    if (misc[1] != ns) return DMMT_E_PPM_SIZE_MISMATCH;
+    if (misc[1] != ns) return dmmt::error_detail(DMMT_E_PPM_SIZE_MISMATCH, 0);
     if (s & 2u) return DMMT_E_VALUE_EXCEEDS_MAX;
     return DMMT_OK;
 }

@@ -96,8 +96,11 @@ extern "C" const char* dmmt_last_error_message(void) {
     case DMMT_E_PPM_INCOMPLETE_PIXEL:
         snprintf(msg, sizeof msg, "Incomplete pixel parsed. Expected 3 components, but got %d.", t_err_detail);
         break;
+    case DMMT_E_PPM_SIZE_MISMATCH:  // (sic, error.rs:39-42)
+        snprintf(msg, sizeof msg, "Nubmer of pixels do not match the size, provided in header");
+        break;
     default:
-        snprintf(msg, sizeof msg, "%s", dmmt_strerror(t_err_code));
+        msg[0] = 0;  // no PPM error on this thread: see dmmt_strerror
     }
     return msg;
 }
@@ -150,7 +153,7 @@ extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) 
     // sb bytes.  A short file claiming a large image allocates no more than that.
     const size_t body = len - tz.i;
     const size_t fit = binary ? body / (size_t)sb : body / 2 + 1;
-    if (binary && fit < npx * 3) return DMMT_E_PPM_SIZE_MISMATCH;
+    if (binary && fit < npx * 3) return error_detail(DMMT_E_PPM_SIZE_MISMATCH, 0);
     const size_t cap = npx * 3 < fit ? npx * 3 : fit;
     uint8_t* buf = (uint8_t*)malloc(cap * (size_t)sb + 1);
     if (!buf) return DMMT_E_OUT_OF_MEMORY;
@@ -190,7 +193,7 @@ extern "C" int dmmt_parse_ppm(const uint8_t* data, size_t len, dmmt_image* img) 
         }
         if (count != npx * 3) {  // ppm.rs:165-175
             free(buf);
-            return DMMT_E_PPM_SIZE_MISMATCH;
+            return error_detail(DMMT_E_PPM_SIZE_MISMATCH, 0);
         }
         if (over) {  // RangeColorFormat::new panics (ppm.rs:155, color.rs:63-65)
             free(buf);

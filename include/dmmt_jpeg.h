@@ -286,7 +286,7 @@ int dmmt_convert_ppm_to_jpeg(dmmt_ctx* ctx, const char* input_path, const char* 
  * (ppm.rs:239-245); PPMFileDoesNotContainRequiredToken / ParsingOfTokenFailed -> the token
  * (0 "P3 Header", 1 "Width Header", 2 "Height Header", 3 "Max Value Header", 4 "Color
  * Component Value", ppm.rs:80-84).  dmmt_last_error_message: the variant's Display text with
- * that payload (error.rs:25-60). */
+ * that payload (error.rs:25-60), "" when the last PPM call on this thread succeeded. */
 int dmmt_last_error_detail(void);
 const char* dmmt_last_error_message(void);
 void dmmt_free(void* p);
