@@ -112,9 +112,12 @@ __device__ __forceinline__ int coef_at(const BlockCoef& b, int k) {
 // Blocks arrive column-major (coef_pos); the walk wants zigzag order: one
 // constant permutation of the 64 halves in registers, 32 word builds.  (Walking
 // the column-major registers directly, coef_at(b, coef_pos(k)), is the same
-// computation, yet that build produced wrong bits at the head of some blocks on
-// MI355X -- the first block of a wave, nondeterministically; this form is exact
-// on the parity suite.)
+// computation.  One round-2 build of that form emitted zeros for the head bits of
+// a wave's first block, differently from run to run; the round-3 study
+// (profiles/r03_kemit_fault_study.md) traced it to code generation -- exact at -O1
+// and without the SDWA peephole, unchanged by waits after every instruction -- not
+// to a race in this kernel.  The current tree is exact either way
+// (DMMT_WALK_COLUMN_MAJOR); tests/test_gpu_regressions.py guards the shape.)
 __device__ __forceinline__ void zigzag_in_registers(BlockCoef& b) {
 #ifdef DMMT_WALK_COLUMN_MAJOR
     return;
@@ -323,6 +326,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             load_block(coef + ep * 64, b);
             zigzag_in_registers(b);
             const int dp = dcdiff[ep];
+            DMMT_TRACE(4);
             const int kp = ((int)(el0 % g.bpm) + p) % g.bpm;
             const bool lum = kp < g.n_luma;
             // the wave's walk stops after the last position any of its blocks uses
@@ -330,6 +334,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             SlotSink ss{sSlot + tid, 0ull, 0, 0};
             walk_block(b, dp, sTab + 512 + (lum ? 0 : 16), sTab + (lum ? 0 : 256), ss, kmax);
             sBits[p] = ss.finish();
+            DMMT_TRACE(5);
         }
     }
     __syncthreads();

@@ -5,7 +5,7 @@ set -o pipefail
 O=$PWD/gpurun_out/fault6
 mkdir -p $O
 cd study_wip
-for v in as_orig as_nop_before as_nop_after; do
+for v in ${VARIANTS:-as_orig as_nop_before as_nop_after}; do
   DMMT_LIB_PATH=$PWD/dmmt-jpeg-encoder_amd/lib_$v/libdmmt_jpeg.so timeout -k 10 200 python scripts/debug_determinism.py --n 4 > $O/$v.log 2>&1
   echo "$v rc=$?"; grep -v amdgpu.ids $O/$v.log
 done

@@ -22,7 +22,8 @@ NAMES = {
     "kernels": {0: "front A colour", 1: "front B rows", 2: "front C cols+quant", 3: "front D store",
                 4: "front E symbols", 5: "front hist flush", 10: "tables 1 hist", 6: "tables merge leafsearch", 7: "tables merge pkgsearch", 8: "tables merge barrier", 11: "tables 2 rank",
                 12: "tables 3 merge", 13: "tables 4 leaves", 14: "tables 5 codes", 15: "tables 6 header"},
-    "entropy": {0: "emit load", 1: "emit walk+scan", 2: "emit windows+store", 3: "emit ff/edges"},
+    "entropy": {0: "emit tables+sort", 4: "emit block load+zigzag", 5: "emit walk", 1: "emit scan",
+                2: "emit windows+store", 3: "emit ff/edges"},
 }
 
 

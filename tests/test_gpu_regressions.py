@@ -1,0 +1,49 @@
+"""Regression tests at the shapes where a past build went wrong.
+
+k_emit "wrong head bits" ("The k_emit fault"): a round-2 build whose
+walk read the column-major coefficient registers directly emitted, run to run,
+zeros in place of the DC code and extra bits of the first block of some waves
+(chunk position 64: its head word shared with the previous wave's last block) at
+8K 4:2:0 q95, synthetic frame 95 -- in the whole path and in the back half from
+the oracle's coefficients alike.  The shape is encoded four times each way here:
+every file must be the oracle's, every time (the fault changed from run to run)."""
+import numpy as np
+import pytest
+
+import dmmt_jpeg
+import oracle
+from conftest import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(300)
+def test_emit_head_bits_8k_q95_repeated(encoder):
+    w, h, sub, q = 7680, 4320, 2, 95
+    luma, chroma = dmmt_jpeg.quality_tables(q)
+    opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
+                                              chroma_table=chroma)
+    rgb = synthetic(w, h, frame=q)
+    coef = oracle.forward(rgb, 255, sub, luma, chroma, threads=8)
+    ref = oracle.encode_coefficients(coef, w, h, sub, luma, chroma)
+    img = dmmt_jpeg.Image.from_array(rgb)
+    for run in range(4):
+        assert encoder.encode(img, opts) == ref, f"whole path, run {run}"
+        assert encoder.encode_coefficients(coef, w, h, opts) == ref, f"back half, run {run}"
+    # and through the device-resident lanes, four frames in flight
+    d_in = encoder.malloc(w * h * 3)
+    stride = (dmmt_jpeg.max_jpeg_bytes(w, h, sub) + 255) // 256 * 256
+    d_out, d_len = encoder.malloc(stride * 4), encoder.malloc(16)
+    try:
+        encoder.h2d(d_in, np.ascontiguousarray(rgb))
+        encoder.set_lanes(4)
+        for i in range(4):
+            encoder.encode_device(d_in, 1, w, h, opts, d_out + i * stride, stride, d_len + 4 * i)
+        encoder.synchronize()
+        lens = np.frombuffer(encoder.d2h(d_len, 16), np.uint32)
+        for i in range(4):
+            assert encoder.d2h(d_out + i * stride, int(lens[i])) == ref, f"lane {i}"
+    finally:
+        encoder.set_lanes(1)
+        for p in (d_in, d_out, d_len):
+            encoder.free(p)
