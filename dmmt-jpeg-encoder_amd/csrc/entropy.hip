@@ -265,6 +265,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     __shared__ uint32_t sBin[65];  // walk order: blocks counted, then started, by last non-zero position
+    __shared__ uint32_t sStart[kEmitThreads];  // bit offset of block t in the chunk
     using OrderT = std::conditional_t<(kEmitThreads > 256), uint16_t, uint8_t>;
     uint32_t* const sBits = sW;                                                      // bit count of block t
     OrderT* const sOrder = reinterpret_cast<OrderT*>(sW + kEmitThreads);               // block walked by thread u
@@ -298,8 +299,8 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     // blocks still has a non-zero coefficient, so the chunk's blocks are handed to
     // the threads sorted by their last non-zero position (k_front's lastnz): at
     // 4K q90 the mean over waves of the last such position falls from 61 to 39.
-    // Thread u walks block sOrder[u] into its own slot u; block t's bits are then
-    // scanned and copied in stream order from slot `mine`.
+    // Thread u walks block sOrder[u] into its own slot u; after the scan (in
+    // stream order) it shifts that slot into the window at the block's offset.
     const int key = valid ? (int)lastnz[e] : 64;
     __syncthreads();
     const uint32_t rank = atomicAdd(&sBin[key], 1u);
@@ -317,10 +318,13 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     }
     __syncthreads();
     DMMT_TRACE(0);
+    int pw = 0;          // the block this thread walks
+    uint32_t wbits = 0;  // and its bits
     {
         // one walk: the block's bits into this thread's private slot, and its bit count
         if (valid) {
             const int p = sOrder[tid];
+            pw = p;
             const long long ep = (long long)frame * g.bpf + el0 + p;
             BlockCoef b;
             load_block(coef + ep * 64, b);
@@ -333,7 +337,8 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             const int kmax = __builtin_amdgcn_readfirstlane((int)sKey[min(64 * wave + 63, nb - 1)]);
             SlotSink ss{sSlot + tid, 0ull, 0, 0};
             walk_block(b, dp, sTab + 512 + (lum ? 0 : 16), sTab + (lum ? 0 : 256), ss, kmax);
-            sBits[p] = ss.finish();
+            wbits = ss.finish();
+            sBits[p] = wbits;
             DMMT_TRACE(5);
         }
     }
@@ -356,6 +361,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     }
     DMMT_TRACE(1);
 
+    sStart[tid] = start;  // (read by the block's walker after the window clear's barrier)
     uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
     const int nw = (int)((total + 31) >> 5);
     const int we1 = total >= 16 ? (int)((total - 16) >> 5) : 0;  // word holding bit total-16
@@ -364,26 +370,31 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         const int wn = min(kEmitWords, nw - w0);
         for (int i = tid; i <= wn; i += kEmitThreads) sW[i] = 0u;  // + the next window's first word
         __syncthreads();
-        if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
-            if (!over) {
-                // shift the slot into place: destination word d of the window image
-                // gets the slot bits that land in it; the first and last word are
-                // shared with the neighbouring blocks (ORed), the rest are this
-                // block's alone
-                const int sh = (int)(start & 31);
-                const int d0 = (int)(start >> 5), d1 = (int)((start + bits - 1) >> 5);
-                const int nsw = (int)((bits + 31) >> 5);
-                for (int d = max(d0, w0); d <= min(d1, w0 + wn); ++d) {
-                    const int k = d - d0;  // slot word feeding the low part (k-1 feeds the high part)
-                    const uint32_t lo = k < nsw ? sSlot[k * kEmitThreads + mine] : 0u;
-                    const uint32_t hi = k > 0 ? sSlot[(k - 1) * kEmitThreads + mine] : 0u;
-                    const uint32_t v = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+        if (!over) {
+            // the walking thread shifts its own slot into place (the wave's slot reads
+            // are consecutive words): destination word d gets ({slot[k-1], slot[k]} >>
+            // sh) for k = d - d0; the first and last word are shared with the
+            // neighbouring blocks (ORed), the rest are this block's alone
+            const uint32_t s0 = wbits ? sStart[pw] : 0u;
+            if (wbits && s0 < (uint32_t)(w0 + wn + 1) * 32u && s0 + wbits > (uint32_t)w0 * 32u) {
+                const int sh = (int)(s0 & 31);
+                const int d0 = (int)(s0 >> 5), d1 = (int)((s0 + wbits - 1) >> 5);
+                const int nsw = (int)((wbits + 31) >> 5);
+                const int da = max(d0, w0), db = min(d1, w0 + wn);
+                uint32_t prev = da > d0 ? sSlot[(da - d0 - 1) * kEmitThreads + tid] : 0u;
+                for (int d = da; d <= db; ++d) {
+                    const int k = d - d0;
+                    const uint32_t cur = k < nsw ? sSlot[k * kEmitThreads + tid] : 0u;
+                    const uint32_t v = __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh);
+                    prev = cur;
                     if (d == d0 || d == d1)
                         atomicOr(&sW[d - w0], v);
                     else
                         sW[d - w0] = v;
                 }
-            } else {
+            }
+        } else if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
+            {
                 // the block again (L2 / MALL) and a second walk straight into the
                 // window: holding it in registers across the scan would halve the
                 // occupancy of this kernel
