@@ -90,7 +90,8 @@ struct dmmt_ctx {
     // host-API staging
     DevBuf in, out, out_len, dct;
     // PPM ingest: file bytes, chunk maps / entry states, status + token count
-    DevBuf ppm_text, ppm_maps, ppm_chunk_in, ppm_counts, ppm_misc;
+    DevBuf ppm_text, ppm_maps, ppm_chunk_in, ppm_misc, ppm_counts;
+    void* ppm_report = nullptr;  // host-mapped report of the comment-free P3 path (24 bytes)
     // uploaded table state
     int lut_maxval = -1, lut_sb = -1;
     uint8_t q_cached[128];
@@ -560,8 +561,11 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
     for (size_t i = 0; i < c->lanes.size(); ++i) destroy_lane(c->lanes[i], i > 0);
     if (c->ev_lane0) (void)hipEventDestroy(c->ev_lane0);
     if (c->ev_caller) (void)hipEventDestroy(c->ev_caller);
-    DevBuf* bufs[] = {&c->lut, &c->qtab, &c->qtab_u8, &c->in, &c->out, &c->out_len, &c->dct};
+    DevBuf* bufs[] = {&c->lut,      &c->qtab,         &c->qtab_u8,  &c->in,       &c->out,     &c->out_len,
+                      &c->dct,      &c->ppm_text,     &c->ppm_maps, &c->ppm_chunk_in, &c->ppm_misc,
+                      &c->ppm_counts};
     for (DevBuf* b : bufs) release(*b);
+    if (c->ppm_report) (void)hipHostFree(c->ppm_report);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -851,7 +855,6 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
     const int sb = h->maxval > 255 ? 2 : 1;
     if (h->body_offset > len) return DMMT_E_INVALID_ARGUMENT;
     if ((rc = ensure(c->ppm_misc, 64, true))) return rc;
-    uint64_t misc[4] = {0, 0, 0, 0};  // PpmMisc: status | status_fast << 32, tokens, flag
     if (h->binary) {  // P6 (extension): raw big-endian samples after the header, as dmmt_parse_ppm
         if (len - h->body_offset < ns * (unsigned long long)sb) return dmmt::error_detail(DMMT_E_PPM_SIZE_MISMATCH, 0);
         HIP_TRY(launch_ppm_p6(d_text + h->body_offset, d_rgb, sb, ns, h->maxval, nullptr, st));
@@ -859,19 +862,39 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
         return DMMT_OK;
     }
     const size_t nch = ppm_chunk_count(d_text, h->body_offset, len);
-    if ((rc = ensure(c->ppm_maps, std::max<size_t>(nch, 1024) * 8))) return rc;
-    if ((rc = ensure(c->ppm_chunk_in, std::max<size_t>(nch, 1024) * 8))) return rc;
-    if ((rc = ensure(c->ppm_counts, ppm_counts_capacity((long long)nch) * 4))) return rc;
-    HIP_TRY(launch_ppm_p3(d_text, h->body_offset, len, (unsigned long long*)c->ppm_maps.p,
-                          (unsigned long long*)c->ppm_chunk_in.p, (uint32_t*)c->ppm_counts.p, c->ppm_misc.p,
-                          d_rgb, sb, ns, h->maxval, st));
-    HIP_TRY(hipMemcpyAsync(misc, c->ppm_misc.p, 24, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    const bool comments = (uint32_t)misc[2] != 0;
-    const uint32_t s = comments ? (uint32_t)misc[0] : (uint32_t)(misc[0] >> 32);
+    uint32_t s = 0;             // 1 a token that does not parse, 2 a sample above maxval
+    unsigned long long n = 0;   // tokens
+    bool comments = true;
+    if (ppm_fast_path(d_text, h->body_offset, len)) {  // two passes, unless the body holds a '#'
+        if ((rc = ensure(c->ppm_counts, ppm_counts_capacity((long long)nch) * 4))) return rc;
+        if ((rc = ensure(c->ppm_chunk_in, std::max<size_t>(nch, 1024) * 8))) return rc;
+        if (!c->ppm_report) HIP_TRY(hipHostMalloc(&c->ppm_report, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        volatile uint32_t* rep = (volatile uint32_t*)c->ppm_report;  // '#' seen, bad, over, -, tokens (u64)
+        for (int i = 0; i < 6; ++i) rep[i] = 0u;                     // (no kernel of this stream is writing it)
+        void* drep = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&drep, c->ppm_report, 0));
+        HIP_TRY(launch_ppm_p3_fast(d_text, h->body_offset, len, (uint32_t*)c->ppm_counts.p,
+                                   (unsigned long long*)c->ppm_chunk_in.p, drep, d_rgb, sb, ns, h->maxval, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        comments = rep[0] != 0u;
+        s = (rep[1] ? 1u : 0u) | (rep[2] ? 2u : 0u);
+        n = (unsigned long long)rep[4] | ((unsigned long long)rep[5] << 32);
+    }
+    if (comments) {  // comments (or a body too short for the fast path): the general path
+        if ((rc = ensure(c->ppm_maps, std::max<size_t>(nch, 1024) * 8))) return rc;
+        if ((rc = ensure(c->ppm_chunk_in, std::max<size_t>(nch, 1024) * 8))) return rc;
+        uint64_t misc[3] = {0, 0, 0};  // PpmMisc: status, tokens, comment flag
+        HIP_TRY(launch_ppm_p3_general(d_text, h->body_offset, len, (unsigned long long*)c->ppm_maps.p,
+                                      (unsigned long long*)c->ppm_chunk_in.p, c->ppm_misc.p, d_rgb, sb, ns, h->maxval,
+                                      st));
+        HIP_TRY(hipMemcpyAsync(misc, c->ppm_misc.p, 24, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        s = (uint32_t)misc[0];
+        n = misc[1];
+    }
     if (s & 1u) return dmmt::error_detail(DMMT_E_PPM_PARSE_TOKEN, 4);  // "Color Component Value"
-    if (misc[1] % 3) return dmmt::error_detail(DMMT_E_PPM_INCOMPLETE_PIXEL, (int)(misc[1] % 3));
-    if (misc[1] != ns) return dmmt::error_detail(DMMT_E_PPM_SIZE_MISMATCH, 0);
+    if (n % 3) return dmmt::error_detail(DMMT_E_PPM_INCOMPLETE_PIXEL, (int)(n % 3));
+    if (n != ns) return dmmt::error_detail(DMMT_E_PPM_SIZE_MISMATCH, 0);
     if (s & 2u) return DMMT_E_VALUE_EXCEEDS_MAX;
     return DMMT_OK;
 }

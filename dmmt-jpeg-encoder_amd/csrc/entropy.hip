@@ -240,6 +240,30 @@ struct SlotSink {
     }
 };
 
+// The walker's copy of its slot (sSlot column tid, nbits bits) into the window
+// image of words [w0, w0 + wn] at chunk bit s0: destination word d gets
+// ({slot[k-1], slot[k]} >> sh) for k = d - d0; the first and last word are shared
+// with the neighbouring blocks (ORed), the rest are this block's alone
+__device__ __forceinline__ void copy_slot(const uint32_t* __restrict__ sSlot, int tid, uint32_t s0, uint32_t nbits,
+                                          uint32_t* sW, int w0, int wn) {
+    if (!nbits || s0 >= (uint32_t)(w0 + wn + 1) * 32u || s0 + nbits <= (uint32_t)w0 * 32u) return;
+    const int sh = (int)(s0 & 31);
+    const int d0 = (int)(s0 >> 5), d1 = (int)((s0 + nbits - 1) >> 5);
+    const int nsw = (int)((nbits + 31) >> 5);
+    const int da = max(d0, w0), db = min(d1, w0 + wn);
+    uint32_t prev = da > d0 ? sSlot[(da - d0 - 1) * kEmitThreads + tid] : 0u;
+    for (int d = da; d <= db; ++d) {
+        const int k = d - d0;
+        const uint32_t cur = k < nsw ? sSlot[k * kEmitThreads + tid] : 0u;
+        const uint32_t v = __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh);
+        prev = cur;
+        if (d == d0 || d == d1)
+            atomicOr(&sW[d - w0], v);
+        else
+            sW[d - w0] = v;
+    }
+}
+
 // 16 bits of an MSB-first word stream starting at bit p (p & 31 taken; words a, b
 // hold bits from (p & ~31))
 __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
@@ -320,6 +344,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     DMMT_TRACE(0);
     int pw = 0;          // the block this thread walks
     uint32_t wbits = 0;  // and its bits
+    bool slot_over = false;
     {
         // one walk: the block's bits into this thread's private slot, and its bit count
         if (valid) {
@@ -338,17 +363,17 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             SlotSink ss{sSlot + tid, 0ull, 0, 0};
             walk_block(b, dp, sTab + 512 + (lum ? 0 : 16), sTab + (lum ? 0 : 256), ss, kmax);
             wbits = ss.finish();
+            slot_over = wbits > (uint32_t)kSlotWords * 32u;
             sBits[p] = wbits;
             DMMT_TRACE(5);
         }
     }
-    __syncthreads();
+    // a block too long for its slot sends the whole chunk down the re-walk path
+    const bool over = __syncthreads_or(slot_over) != 0;
     const uint32_t bits = valid ? sBits[tid] : 0u;
     const int k = valid ? ((int)(el0 % g.bpm) + tid) % g.bpm : 0;
     const bool lum_t = k < g.n_luma;
-    // offsets inside the chunk by a workgroup scan; a block too long for its slot
-    // sends the whole chunk down the re-walk path
-    const bool over = __syncthreads_or(bits > (uint32_t)kSlotWords * 32u) != 0;
+    // offsets inside the chunk by a workgroup scan
     const uint32_t incl = wave_incl_scan_full_u32(bits);
     if (lane == 63) sWave[wave] = incl;
     __syncthreads();
@@ -372,27 +397,8 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         __syncthreads();
         if (!over) {
             // the walking thread shifts its own slot into place (the wave's slot reads
-            // are consecutive words): destination word d gets ({slot[k-1], slot[k]} >>
-            // sh) for k = d - d0; the first and last word are shared with the
-            // neighbouring blocks (ORed), the rest are this block's alone
-            const uint32_t s0 = wbits ? sStart[pw] : 0u;
-            if (wbits && s0 < (uint32_t)(w0 + wn + 1) * 32u && s0 + wbits > (uint32_t)w0 * 32u) {
-                const int sh = (int)(s0 & 31);
-                const int d0 = (int)(s0 >> 5), d1 = (int)((s0 + wbits - 1) >> 5);
-                const int nsw = (int)((wbits + 31) >> 5);
-                const int da = max(d0, w0), db = min(d1, w0 + wn);
-                uint32_t prev = da > d0 ? sSlot[(da - d0 - 1) * kEmitThreads + tid] : 0u;
-                for (int d = da; d <= db; ++d) {
-                    const int k = d - d0;
-                    const uint32_t cur = k < nsw ? sSlot[k * kEmitThreads + tid] : 0u;
-                    const uint32_t v = __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh);
-                    prev = cur;
-                    if (d == d0 || d == d1)
-                        atomicOr(&sW[d - w0], v);
-                    else
-                        sW[d - w0] = v;
-                }
-            }
+            // are consecutive words)
+            copy_slot(sSlot, tid, wbits ? sStart[pw] : 0u, wbits, sW, w0, wn);
         } else if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
             {
                 // the block again (L2 / MALL) and a second walk straight into the

@@ -43,15 +43,22 @@ hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_
 hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
                              uint32_t* out_len, hipStream_t st);
 // P3 body decoding (ppm_device.hip): text [body_offset, len) -> nsamples samples of
-// sample_bytes each.  misc (32 bytes, PpmMisc): u32 status of the general path, u32
-// status of the comment-free path (bits: 1 parse error, 2 sample above maxval),
-// u64 tokens found, u32 comment flag.  With n = ppm_chunk_count(...): maps and
-// chunk_in 8 max(n, 1024) bytes each, counts 4 ppm_counts_capacity(n) bytes.
+// sample_bytes each.  The comment-free path (when ppm_fast_path) runs first and
+// writes its report into host-mapped memory (24 bytes, zeroed by the caller before
+// the launch: u32 '#' seen, u32 parse error, u32 sample above maxval, u32, u64 tokens
+// found); counts: 4 ppm_counts_capacity(n) bytes, row_base 8 * 1024 bytes.  If it
+// saw a '#', the general path redoes the body: misc (device, 24 bytes: u32 status
+// (1 parse error, 2 sample above maxval), u32, u64 tokens found), maps and chunk_in
+// 8 max(n, 1024) bytes each (n = ppm_chunk_count(...)).
 size_t ppm_chunk_count(const uint8_t* text, size_t body_offset, size_t len);
 size_t ppm_counts_capacity(long long nch);
-hipError_t launch_ppm_p3(const uint8_t* text, size_t body_offset, size_t len, unsigned long long* maps,
-                         unsigned long long* chunk_in, uint32_t* counts, void* misc, void* out, int sample_bytes,
-                         unsigned long long nsamples, uint32_t maxval, hipStream_t st);
+bool ppm_fast_path(const uint8_t* text, size_t body_offset, size_t len);
+hipError_t launch_ppm_p3_fast(const uint8_t* text, size_t body_offset, size_t len, uint32_t* counts,
+                              unsigned long long* row_base, void* report, void* out, int sample_bytes,
+                              unsigned long long nsamples, uint32_t maxval, hipStream_t st);
+hipError_t launch_ppm_p3_general(const uint8_t* text, size_t body_offset, size_t len, unsigned long long* maps,
+                                 unsigned long long* chunk_in, void* misc, void* out, int sample_bytes,
+                                 unsigned long long nsamples, uint32_t maxval, hipStream_t st);
 // P6 samples (big-endian u16 or u8) already in device memory -> host-endian samples
 // (maxval and status unused: the encoder checks the range, as for dmmt_parse_ppm)
 hipError_t launch_ppm_p6(const uint8_t* samples, void* out, int sample_bytes, unsigned long long nsamples,

@@ -8,16 +8,17 @@
 // \r) ends a token; every token must parse as a u16 (Rust `str::parse::<u16>`:
 // an optional '+', then decimal digits, value <= 65535).
 //
-// Two paths, chosen on the device (no host round trip):
+// Two paths:
 //  comment-free bodies (no '#' after the header: every P3 writer's output), 16 KB
 //  chunks, 64 bytes per thread, classified by SWAR word arithmetic --
 //   k_ppm_count  every chunk's token count (a token starts at each token byte
-//                after whitespace); raises the comment flag on any '#'
-//   k_ppm_carry  one workgroup: exclusive sums of the counts over 1024 rows
+//                after whitespace); reports a '#' anywhere
+//   k_ppm_rows   one workgroup: exclusive sums of the counts over 1024 rows
 //   k_ppm_fast   every chunk: its tokens parsed token by token (SWAR digits),
 //                staged in LDS in token order, stored coalesced
-//  bodies with comments (flag raised; otherwise these are empty launches), 4 KB
-//  chunks, 16 bytes per thread --
+//  The host reads the path's report (host-mapped memory, no copy) after it; a '#'
+//  sends the body down the general path, which a body shorter than 96 bytes takes
+//  from the start -- 4 KB chunks, 16 bytes per thread:
 //   k_ppm_maps   every chunk's transition map: for each of the 4 states the text
 //                can be in where the chunk starts (inside a comment?, last kept
 //                byte a token byte?) the state at its end and the tokens starting
@@ -355,16 +356,24 @@ __device__ __forceinline__ void put_sample(Out* out, unsigned long long idx, uns
     if (idx < nsamples) out[idx] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
 }
 
-// misc words (zeroed per call): status of the general path, status of the fast
-// path, token count, comment flag
+// misc words of the general path (zeroed per call): its status (1 parse error, 2
+// sample above maxval), the token count
 struct PpmMisc {
-    uint32_t status, status_fast;
+    uint32_t status, pad0;
     unsigned long long tokens;
-    uint32_t flag, pad;
+    uint32_t pad1, pad2;
+};
+
+// What the comment-free path reports, in host-mapped memory (plain stores: every
+// writer of a word stores the same value; the host reads it after the stream's
+// work, so no copy is needed)
+struct PpmReport {
+    uint32_t comment, bad, over, pad;
+    unsigned long long tokens;
 };
 
 __global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* __restrict__ counts,
-                                                           PpmMisc* __restrict__ misc) {
+                                                           PpmReport* __restrict__ rep) {
     __shared__ uint32_t sRed[kPpmThreads / 64];
     const int tid = threadIdx.x;
     const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
@@ -377,7 +386,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* 
         uint32_t c = 0;
         for (int q = 0; q < kPpmThreads / 64; ++q) c += sRed[q];
         counts[blockIdx.x] = c;
-        if (hash) atomicOr(&misc->flag, 1u);
+        if (hash) reinterpret_cast<volatile uint32_t*>(&rep->comment)[0] = 1u;
     }
 }
 
@@ -399,7 +408,7 @@ __device__ __forceinline__ uint32_t fast_token(int r, uint32_t lo, uint32_t hi, 
 }
 
 template <typename Out>
-__global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __restrict__ misc,
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* __restrict__ rep,
                                                           const uint32_t* __restrict__ counts,
                                                           const unsigned long long* __restrict__ row_base,
                                                           long long per, Out* __restrict__ out,
@@ -409,7 +418,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
     // at most one token per two bytes, staged at the output's 16-byte alignment
     __shared__ __attribute__((aligned(16))) Out sOut[kFastChunk / 2 + 16 / sizeof(Out)];
     __shared__ uint32_t sWin[kPpmThreads * 17];  // each lane's 16 window words + the next one
-    if (misc->flag != 0u) return;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
     // the first token's index: the row's base + the counts before this chunk in
@@ -485,20 +493,18 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmMisc* __
                 *reinterpret_cast<Out*>(oa + i) = *reinterpret_cast<const Out*>(so + i);
         }
     }
-    if (bad) atomicOr(&misc->status_fast, 1u);
-    if (over) atomicOr(&misc->status_fast, 2u);
+    if (bad) reinterpret_cast<volatile uint32_t*>(&rep->bad)[0] = 1u;
+    if (over) reinterpret_cast<volatile uint32_t*>(&rep->over)[0] = 1u;
 }
 
 // ---------------------------------------------------------------- general path
-// Only when the body holds a '#' (misc->flag); otherwise each is an empty launch
-// of kPpmGeneralGrid workgroups.
+// Only when the body holds a '#' (or is shorter than 96 bytes): kPpmGeneralGrid
+// workgroups, each looping over chunks.
 constexpr int kPpmGeneralGrid = 256;
 
 // every chunk's transition map
-__global__ __launch_bounds__(kPpmThreads) void k_ppm_maps(PpmText t, const PpmMisc* __restrict__ misc,
-                                                          unsigned long long* __restrict__ maps) {
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_maps(PpmText t, unsigned long long* __restrict__ maps) {
     __shared__ unsigned long long sWave[kPpmThreads / 64];
-    if (misc->flag == 0u) return;
     for (long long k = blockIdx.x; k < t.nch; k += gridDim.x) {
         const long long pos = k * kPpmChunk + (long long)threadIdx.x * kPpmWin;
         PpmWin W;
@@ -545,44 +551,46 @@ __device__ __forceinline__ WideMap widen(unsigned long long m) {
     return w;
 }
 
-// chunk_in[k] = entry state << 62 | index of the chunk's first token; the token count
-__global__ __launch_bounds__(kPpmCarryThreads) void k_ppm_carry(const uint32_t* __restrict__ counts,
-                                                                const unsigned long long* __restrict__ maps,
-                                                                long long nch, long long nfast, long long rper,
-                                                                PpmMisc* __restrict__ misc,
+// comment-free path: thread t's row = chunks [t*rper, (t+1)*rper) (rper a multiple
+// of 4: 16-byte loads; the counts buffer is padded), its exclusive sum ->
+// row_base[t]; k_ppm_fast adds the counts before it within its row
+__global__ __launch_bounds__(kPpmCarryThreads) void k_ppm_rows(const uint32_t* __restrict__ counts, long long nfast,
+                                                               long long rper, PpmReport* __restrict__ rep,
+                                                               unsigned long long* __restrict__ row_base) {
+    __shared__ unsigned long long sSum[kPpmCarryThreads / 64];
+    const int t = threadIdx.x;
+    const long long r0 = (long long)t * rper;
+    unsigned long long s = 0;
+    for (long long kb = r0; kb < r0 + rper; kb += 16) {
+        uint4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = *reinterpret_cast<const uint4*>(counts + kb + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long long k = kb + 4 * u;
+            s += (k < nfast ? c[u].x : 0u) + (k + 1 < nfast ? c[u].y : 0u) + (k + 2 < nfast ? c[u].z : 0u) +
+                 (k + 3 < nfast ? c[u].w : 0u);
+            if (kb + 4 * u + 4 >= r0 + rper) break;
+        }
+    }
+    const unsigned long long inc = wave_incl_scan_full_u64(s);
+    if (lane_id() == 63) sSum[t >> 6] = inc;
+    __syncthreads();
+    unsigned long long base = inc - s;
+    for (int q = 0; q < (t >> 6); ++q) base += sSum[q];
+    row_base[t] = base;
+    if (t == kPpmCarryThreads - 1) reinterpret_cast<volatile unsigned long long*>(&rep->tokens)[0] = base + s;
+}
+
+// general path: chunk_in[k] = entry state << 62 | index of the chunk's first token;
+// the token count
+__global__ __launch_bounds__(kPpmCarryThreads) void k_ppm_carry(const unsigned long long* __restrict__ maps,
+                                                                long long nch, PpmMisc* __restrict__ misc,
                                                                 unsigned long long* __restrict__ chunk_in) {
     __shared__ WideMap sScan[kPpmCarryThreads];
     const int t = threadIdx.x;
     const long long per = (nch + kPpmCarryThreads - 1) / kPpmCarryThreads;
     const long long k0 = min((long long)t * per, nch), k1 = min(k0 + per, nch);
-    if (misc->flag == 0u) {
-        // comment-free: thread t's row = chunks [t*rper, (t+1)*rper) (rper a multiple
-        // of 4: 16-byte loads; the counts buffer is padded), its exclusive sum ->
-        // row_base[t]; k_ppm_fast adds the counts before it within its row
-        unsigned long long* sSum = reinterpret_cast<unsigned long long*>(sScan);
-        const long long r0 = (long long)t * rper;
-        unsigned long long s = 0;
-        for (long long kb = r0; kb < r0 + rper; kb += 16) {
-            uint4 c[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) c[u] = *reinterpret_cast<const uint4*>(counts + kb + 4 * u);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const long long k = kb + 4 * u;
-                s += (k < nfast ? c[u].x : 0u) + (k + 1 < nfast ? c[u].y : 0u) + (k + 2 < nfast ? c[u].z : 0u) +
-                     (k + 3 < nfast ? c[u].w : 0u);
-                if (kb + 4 * u + 4 >= r0 + rper) break;
-            }
-        }
-        const unsigned long long inc = wave_incl_scan_full_u64(s);
-        if (lane_id() == 63) sSum[t >> 6] = inc;
-        __syncthreads();
-        unsigned long long base = inc - s;
-        for (int q = 0; q < (t >> 6); ++q) base += sSum[q];
-        chunk_in[t] = base;  // the row bases
-        if (t == kPpmCarryThreads - 1) misc->tokens = base + s;
-        return;
-    }
     WideMap m = wide_identity();
     for (long long k = k0; k < k1; ++k) m = wide_compose(m, widen(maps[k]));
     sScan[t] = m;
@@ -613,7 +621,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_parse(PpmText t, PpmMisc* _
                                                            uint32_t maxval) {
     __shared__ unsigned long long sWave[kPpmThreads / 64];
     __shared__ __attribute__((aligned(16))) uint8_t sText[kPpmChunk + kPpmTail];
-    if (misc->flag == 0u) return;
     const int tid = threadIdx.x;
     uint32_t bad = 0, over = 0;
     for (long long k = blockIdx.x; k < t.nch; k += gridDim.x) {
@@ -685,42 +692,50 @@ size_t ppm_chunk_count(const uint8_t* text, size_t body_offset, size_t len) {
     return (size_t)ppm_chunks(text, body_offset, len, &t);
 }
 
-hipError_t launch_ppm_p3(const uint8_t* text, size_t body_offset, size_t len, unsigned long long* maps,
-                         unsigned long long* chunk_in, uint32_t* counts, void* misc, void* out, int sample_bytes,
-                         unsigned long long nsamples, uint32_t maxval, hipStream_t st) {
+bool ppm_fast_path(const uint8_t* text, size_t body_offset, size_t len) {
+    PpmText t;
+    // the comment-free kernels read at clamped addresses: texts of fewer than 96
+    // bytes take the general path
+    return ppm_chunks(text, body_offset, len, &t) > 0 && t.len - t.safe >= 96;
+}
+
+hipError_t launch_ppm_p3_fast(const uint8_t* text, size_t body_offset, size_t len, uint32_t* counts,
+                              unsigned long long* row_base, void* report, void* out, int sample_bytes,
+                              unsigned long long nsamples, uint32_t maxval, hipStream_t st) {
+    PpmText t;
+    if (ppm_chunks(text, body_offset, len, &t) == 0) return hipSuccess;
+    PpmReport* r = reinterpret_cast<PpmReport*>(report);
+    const unsigned nfast = (unsigned)t.nfast;
+    const long long rper = ppm_row_chunks(t.nfast);
+    hipLaunchKernelGGL(k_ppm_count, dim3(nfast), dim3(kPpmThreads), 0, st, t, counts, r);
+    hipLaunchKernelGGL(k_ppm_rows, dim3(1), dim3(kPpmCarryThreads), 0, st, (const uint32_t*)counts, t.nfast, rper, r,
+                       row_base);
+    if (sample_bytes == 1)
+        hipLaunchKernelGGL(k_ppm_fast<uint8_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, r, (const uint32_t*)counts,
+                           (const unsigned long long*)row_base, rper, (uint8_t*)out, nsamples, maxval);
+    else
+        hipLaunchKernelGGL(k_ppm_fast<uint16_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, r, (const uint32_t*)counts,
+                           (const unsigned long long*)row_base, rper, (uint16_t*)out, nsamples, maxval);
+    return hipGetLastError();
+}
+
+hipError_t launch_ppm_p3_general(const uint8_t* text, size_t body_offset, size_t len, unsigned long long* maps,
+                                 unsigned long long* chunk_in, void* misc, void* out, int sample_bytes,
+                                 unsigned long long nsamples, uint32_t maxval, hipStream_t st) {
     PpmText t;
     PpmMisc* m = reinterpret_cast<PpmMisc*>(misc);
     hipError_t e = hipMemsetAsync(misc, 0, sizeof(PpmMisc), st);
     if (e != hipSuccess || ppm_chunks(text, body_offset, len, &t) == 0) return e;
     const unsigned gen = (unsigned)(t.nch < kPpmGeneralGrid ? t.nch : kPpmGeneralGrid);
-    const unsigned nfast = (unsigned)t.nfast;
-    const long long rper = ppm_row_chunks(t.nfast);
-    // the comment-free kernels read at clamped addresses: texts of fewer than 96
-    // bytes go down the general path instead (flag preset)
-    const bool tiny = t.len - t.safe < 96;
-    if (tiny) {
-        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&m->flag), 1, 1, st)) != hipSuccess) return e;
-    } else {
-        hipLaunchKernelGGL(k_ppm_count, dim3(nfast), dim3(kPpmThreads), 0, st, t, counts, m);
-    }
-    hipLaunchKernelGGL(k_ppm_maps, dim3(gen), dim3(kPpmThreads), 0, st, t, (const PpmMisc*)m, maps);
-    hipLaunchKernelGGL(k_ppm_carry, dim3(1), dim3(kPpmCarryThreads), 0, st, (const uint32_t*)counts,
-                       (const unsigned long long*)maps, t.nch, t.nfast, rper, m, chunk_in);
-    if (sample_bytes == 1) {
-        if (!tiny)
-            hipLaunchKernelGGL(k_ppm_fast<uint8_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, m,
-                               (const uint32_t*)counts, (const unsigned long long*)chunk_in, rper, (uint8_t*)out,
-                               nsamples, maxval);
+    hipLaunchKernelGGL(k_ppm_maps, dim3(gen), dim3(kPpmThreads), 0, st, t, maps);
+    hipLaunchKernelGGL(k_ppm_carry, dim3(1), dim3(kPpmCarryThreads), 0, st, (const unsigned long long*)maps, t.nch, m,
+                       chunk_in);
+    if (sample_bytes == 1)
         hipLaunchKernelGGL(k_ppm_parse<uint8_t>, dim3(gen), dim3(kPpmThreads), 0, st, t, m,
                            (const unsigned long long*)chunk_in, (uint8_t*)out, nsamples, maxval);
-    } else {
-        if (!tiny)
-            hipLaunchKernelGGL(k_ppm_fast<uint16_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, m,
-                               (const uint32_t*)counts, (const unsigned long long*)chunk_in, rper, (uint16_t*)out,
-                               nsamples, maxval);
+    else
         hipLaunchKernelGGL(k_ppm_parse<uint16_t>, dim3(gen), dim3(kPpmThreads), 0, st, t, m,
                            (const unsigned long long*)chunk_in, (uint16_t*)out, nsamples, maxval);
-    }
     return hipGetLastError();
 }
 
