@@ -171,6 +171,85 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
         dist.destroy_process_group()
 
 
+def run_inproc(args, emit, make_group):
+    """`--inproc`: the multi-GPU path a caller of the C ABI uses (one process, no
+    torch.distributed): dmmt_ctx_create_multi over the device ids, every member
+    with its own input frames in its own HBM, each step one dmmt_encode_device_multi
+    call that enqueues one batch of frames per member (frames round-robin over the
+    GPUs, the reference's thread-pool fan-out of lib.rs:62 / cosine_transform.rs:
+    55-73 turned into one host thread per GPU).  Independent frames: weak scaling,
+    value = all members' pixels / elapsed."""
+    ids = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    w, h, sub, quality, fps = CONFIGS[args.config]
+    luma, chroma = dmmt_jpeg.quality_tables(quality)
+    opts = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
+                                               chroma_table=chroma)
+    grp = make_group(ids)
+    n = grp.num_devices()
+    mem = [grp.member_encoder(i) for i in range(n)]
+    frame_bytes = w * h * 3
+    slot_bytes = frame_bytes * fps
+    # per member enough distinct input slots to stream past its device's Infinity
+    # Cache (members sharing one GPU share it: the same count per GPU in total)
+    per_dev = {d: ids.count(d) for d in ids}
+    nslots = args.distinct_frames if args.distinct_frames > 0 else max(
+        2, -(-(MALL_BYTES // slot_bytes + 2) // max(per_dev.values())))
+    out_stride = (dmmt_jpeg.max_jpeg_bytes(w, h, sub) + 255) // 256 * 256
+    lanes = max(1, args.lanes)
+    bufs = []
+    for i, m in enumerate(mem):
+        d_in = [m.malloc(slot_bytes) for _ in range(nslots)]
+        d_out = [m.malloc(out_stride * fps) for _ in range(lanes)]
+        d_len = [m.malloc(4 * fps) for _ in range(lanes)]
+        for k in range(nslots):
+            m.fill_synthetic(d_in[k], w, h, fps, first_frame=(i * nslots + k) * fps)
+        bufs.append((d_in, d_out, d_len))
+
+    def frames(step):
+        fs = []
+        for d_in, d_out, d_len in bufs:
+            f = dmmt_jpeg.DmmtDeviceFrames()
+            f.d_rgb, f.frame_stride, f.n_frames = d_in[step % nslots], frame_bytes, fps
+            f.width, f.height, f.maxval, f.sample_bytes = w, h, 255, 1
+            f.d_out, f.out_stride, f.d_out_len = d_out[step % lanes], out_stride, d_len[step % lanes]
+            fs.append(f)
+        return fs
+
+    grp.set_lanes(lanes)
+    for i in range(args.warmup):
+        grp.encode_device_multi(frames(i), opts)
+    grp.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        grp.encode_device_multi(frames(i), opts)
+    grp.synchronize()
+    elapsed = time.perf_counter() - t0
+    lens = np.frombuffer(mem[0].d2h(bufs[0][2][0], 4 * fps), np.uint32)
+    ngpu = len(set(ids))
+    value = n * w * h * fps * args.steps / elapsed / 1e6
+    line = {
+        "metric": "Mpixel/s encoded (4K PPM, q=90)" if args.config == "4k444q90" else f"Mpixel/s encoded ({args.config})",
+        "value": round(value, 2), "unit": "Mpixel/s", "n_gpus": ngpu, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {
+            "workload": f"{w}x{h} synthetic RGB u8, {['4:4:4', '4:2:2', '4:2:0'][sub]}, IJG quality {quality}, "
+                        f"{fps} frame(s) per step per member, pixels in HBM -> JPEG files in HBM, one process: "
+                        f"dmmt_ctx_create_multi({ids}), one dmmt_encode_device_multi call per step",
+            "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
+            "frames_per_step": fps * n, "members": n, "device_ids": ids, "mean_jpeg_bytes": float(lens.mean()),
+            "parallelism": f"independent frames x{n} members on {ngpu} GPU(s), in-process C-ABI group",
+            "lanes": lanes, "input_slots_per_member": nslots,
+        },
+        "roofline": None, "cpu_baseline": None,
+    }
+    emit(json.dumps(line))
+    for m, (d_in, d_out, d_len) in zip(mem, bufs):
+        for p in d_in + d_out + d_len:
+            m.free(p)
+    grp.close()
+
+
 def p3_bytes(rgb, maxval=255, sep=b" "):
     """a P3 file of an (h, w, 3) uint8 image, built vectorised: every sample in decimal
     followed by one separator byte (the ingest workload of --ppm and its tests)"""
@@ -188,11 +267,9 @@ def p3_bytes(rgb, maxval=255, sep=b" "):
     return b"P3\n%d %d\n%d\n" % (w, h, maxval) + body.tobytes()
 
 
-def ppm_ingest(enc, w, h, steps):
-    """SURVEY.md 8(f) row 1, timed apart from the encode (8(d)): one w x h frame of
-    the synthetic workload as a P3 file (one space after every sample) in HBM ->
-    its u8 samples in HBM, dmmt_decode_ppm_device per step (which synchronises).
-    Algorithmic bytes: the file read once + the samples written once."""
+def _p3_in_hbm(enc, w, h):
+    """one w x h frame of the synthetic workload as a P3 file in HBM: (rgb, text,
+    header, d_text, d_rgb)"""
     d_rgb = enc.malloc(w * h * 3)
     enc.fill_synthetic(d_rgb, w, h, 1)
     enc.synchronize()
@@ -201,6 +278,15 @@ def ppm_ingest(enc, w, h, steps):
     hdr = dmmt_jpeg.parse_ppm_header(text)
     d_text = enc.malloc(len(text))
     enc.h2d(d_text, np.frombuffer(text, np.uint8))
+    return rgb, text, hdr, d_text, d_rgb
+
+
+def ppm_ingest(enc, w, h, steps):
+    """SURVEY.md 8(f) row 1, timed apart from the encode (8(d)): one w x h frame of
+    the synthetic workload as a P3 file (one space after every sample) in HBM ->
+    its u8 samples in HBM, dmmt_decode_ppm_device per step (which synchronises).
+    Algorithmic bytes: the file read once + the samples written once."""
+    rgb, text, hdr, d_text, d_rgb = _p3_in_hbm(enc, w, h)
     for _ in range(3):
         enc.decode_ppm_device(d_text, len(text), hdr, d_rgb)
     t0 = time.perf_counter()
@@ -215,6 +301,38 @@ def ppm_ingest(enc, w, h, steps):
             "ms": round(dt * 1e3, 4), "mpixel_per_s": round(w * h / dt / 1e6, 1),
             "achieved_gbs": round(algo / dt / 1e9, 1), "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4),
             "algorithmic_bytes": algo, "samples_match": ok}
+
+
+def ppm_to_jpeg(enc, w, h, opts, opt_c, steps):
+    """The reference's product path (convert_ppm_to_jpeg, lib.rs:59-77) minus the
+    file I/O: one w x h synthetic frame as P3 text in HBM -> its JPEG file in HBM,
+    one file at a time -- dmmt_decode_ppm_device (which synchronises to read its
+    report), then dmmt_encode_device and a synchronisation.  Algorithmic bytes: the
+    text read once + the JPEG written once."""
+    rgb, text, hdr, d_text, d_rgb = _p3_in_hbm(enc, w, h)
+    cap = (dmmt_jpeg.max_jpeg_bytes(w, h, int(opts.chroma_subsampling_preset)) + 255) // 256 * 256
+    d_out, d_len = enc.malloc(cap), enc.malloc(4)
+    enc.set_lanes(1)
+
+    def one():
+        enc.decode_ppm_device(d_text, len(text), hdr, d_rgb)
+        enc.encode_device(d_rgb, 1, w, h, None, d_out, cap, d_len, frame_stride=w * h * 3, opt_c=opt_c)
+        enc.synchronize()
+    for _ in range(3):
+        one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = (time.perf_counter() - t0) / steps
+    n = int(np.frombuffer(enc.d2h(d_len, 4), np.uint32)[0])
+    for p in (d_text, d_rgb, d_out, d_len):
+        enc.free(p)
+    algo = len(text) + n
+    return {"workload": f"{w}x{h} P3 text ({len(text)} B) in HBM -> JPEG file ({n} B) in HBM, one file at a time "
+                        f"(decode_ppm_device + encode_device + synchronize per file)",
+            "ms": round(dt * 1e3, 4), "mpixel_per_s": round(w * h / dt / 1e6, 1),
+            "achieved_gbs": round(algo / dt / 1e9, 1), "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes": algo}
 
 
 def available_parallelism():
@@ -345,9 +463,30 @@ def kernel_roofline(prof, algo_bytes, frames_per_launch, pmc):
     return out
 
 
-def main(argv=None, make_encoder=None, emit=None):
-    """The bench; `make_encoder(local_rank)` and `emit(line)` are test seams
-    (tests/test_bench_dist.py drives the N>1 path with gloo on CPU)."""
+def path_roofline(algo_bytes, achieved, step_s, pmc):
+    """the whole step against both ceilings: the HBM fraction of the
+    step's algorithmic bytes, and the issue ceiling -- the VALU wave-instructions all
+    kernels of a step issue (PMC, profiles/pmc_<config>.json) over the step time
+    against the measured 1.003 T wave-instructions/s (tools/pk_rate.hip)"""
+    out = {"algorithmic_bytes_per_step": round(algo_bytes), "achieved": round(achieved, 1),
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "valu_wave_insts": None, "salu_wave_insts": None,
+           "valu_frac": None}
+    ks = {n: k for n, k in (pmc or {}).get("kernels", {}).items() if n in KERNELS.values()}  # the step's kernels
+    if len(ks) == len(KERNELS) and all(k.get("SQ_INSTS_VALU") is not None for k in ks.values()):
+        valu = sum(k["SQ_INSTS_VALU"] for k in ks.values())
+        out["valu_wave_insts"] = round(valu)
+        out["valu_frac"] = round(valu / step_s / VALU_PEAK_PER_S, 4)
+        if all(k.get("SQ_INSTS_SALU") is not None for k in ks.values()):
+            out["salu_wave_insts"] = round(sum(k["SQ_INSTS_SALU"] for k in ks.values()))
+        out["valu_frac_def"] = ("sum over the step's kernels of PMC SQ_INSTS_VALU / step time / "
+                                f"{VALU_PEAK_PER_S:.4g} wave-instructions/s")
+    return out
+
+
+def main(argv=None, make_encoder=None, emit=None, make_group=None):
+    """The bench; `make_encoder(local_rank)`, `make_group(device_ids)` and
+    `emit(line)` are test seams (tests/test_bench_dist.py drives the N>1 path with
+    gloo on CPU, and the --inproc path with a stand-in group)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -364,8 +503,18 @@ def main(argv=None, make_encoder=None, emit=None):
                     help="striped configs, N>1: every step also sends the stripes to one file on rank 0 (RCCL p2p)")
     ap.add_argument("--lanes", type=int, default=4,
                     help="pipeline lanes: consecutive steps overlap on this many workspaces/streams (1 = serial)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="one process drives all GPUs through the C ABI's multi-GPU context (dmmt_ctx_create_multi)")
+    ap.add_argument("--devices", default="",
+                    help="--inproc: comma-separated device ids of the members (default 0..gpus-1; repeats allowed)")
     args = ap.parse_args(argv)
     emit = emit or (lambda line: print(line, flush=True))
+    if args.inproc:
+        if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+            raise SystemExit("bench: --inproc drives every GPU from one process; do not launch it per rank")
+        if args.config not in CONFIGS:
+            raise SystemExit("bench: --inproc runs the independent-frame configs")
+        return run_inproc(args, emit, make_group or (lambda ids: dmmt_jpeg.Encoder(devices=ids)))
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # no launcher: start the ranks here
         return spawn_ranks(list(argv if argv is not None else sys.argv[1:]), args.gpus, make_encoder, emit)
@@ -470,6 +619,7 @@ def main(argv=None, make_encoder=None, emit=None):
         dom = max(kern, key=lambda k: kern[k]["avg_launch_us"]) if kern else None
         d = kern.get(dom, {})
         ingest = ppm_ingest(enc, w, h, args.ppm_steps) if args.ppm_steps > 0 else None
+        ppm_jpeg = ppm_to_jpeg(enc, w, h, opts, opt_c, args.ppm_steps) if args.ppm_steps > 0 and fps == 1 else None
         cpu = None
         if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
             from oracle.synth import synthetic  # numpy twin of the device generator
@@ -519,12 +669,12 @@ def main(argv=None, make_encoder=None, emit=None):
                 "algorithmic_bytes_per_launch": round(algo_bytes),
                 "algorithmic_bytes_def": "SURVEY 8(d): 3 B/px RGB in + JPEG bytes out, per frame, x frames per launch",
                 "kernels": kern,
-                "path": {"algorithmic_bytes_per_step": round(algo_bytes), "achieved": round(path_achieved, 1),
-                         "frac": round(path_achieved / HBM_PEAK_GBS, 4)},
+                "path": path_roofline(algo_bytes, path_achieved, elapsed / args.steps, pmc),
                 "pmc_source": f"profiles/pmc_{args.config}.json" if pmc else None,
             },
             "cpu_baseline": cpu,
             "ppm_ingest": ingest,
+            "ppm_to_jpeg": ppm_jpeg,
         }
         emit(json.dumps(line))
     for p in d_in + d_out + d_len:

@@ -748,7 +748,10 @@ extern "C" int dmmt_jpeg_encode_striped(dmmt_ctx* c, const dmmt_image* img, cons
 extern "C" int dmmt_encode_device_multi(dmmt_ctx* c, const dmmt_device_frames* frames, int n,
                                         const dmmt_options* opt) {
     if (!c || !frames || n < 1 || n > dmmt_ctx_num_devices(c)) return DMMT_E_INVALID_ARGUMENT;
-    if (!c->group) return dmmt_encode_device(c, frames, opt, nullptr);
+    if (!c->group) {  // n_frames 0: no frames for this member (as group_encode_device)
+        if (frames[0].n_frames <= 0) return DMMT_OK;
+        return dmmt_encode_device(c, frames, opt, nullptr);
+    }
     return dmmt::group_encode_device(c->group, frames, n, opt);
 }
 
@@ -851,6 +854,7 @@ extern "C" int dmmt_dct_transform(dmmt_ctx* c, float* blocks, size_t len) {
 static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt_ppm_header* h, void* d_rgb,
                       hipStream_t st) {
     int rc;
+    dmmt::error_detail(DMMT_OK, 0);  // the payload of this call's error only (empty on success)
     const unsigned long long ns = (unsigned long long)h->width * h->height * 3ull;
     const int sb = h->maxval > 255 ? 2 : 1;
     if (h->body_offset > len) return DMMT_E_INVALID_ARGUMENT;
@@ -869,15 +873,17 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
         if ((rc = ensure(c->ppm_counts, ppm_counts_capacity((long long)nch) * 4))) return rc;
         if ((rc = ensure(c->ppm_chunk_in, std::max<size_t>(nch, 1024) * 8))) return rc;
         if (!c->ppm_report) HIP_TRY(hipHostMalloc(&c->ppm_report, 64, hipHostMallocMapped | hipHostMallocCoherent));
-        volatile uint32_t* rep = (volatile uint32_t*)c->ppm_report;  // '#' seen, bad, over, -, tokens (u64)
+        volatile uint32_t* rep = (volatile uint32_t*)c->ppm_report;  // -, bad, over, -, tokens (u64)
         for (int i = 0; i < 6; ++i) rep[i] = 0u;                     // (no kernel of this stream is writing it)
         void* drep = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&drep, c->ppm_report, 0));
         HIP_TRY(launch_ppm_p3_fast(d_text, h->body_offset, len, (uint32_t*)c->ppm_counts.p,
                                    (unsigned long long*)c->ppm_chunk_in.p, drep, d_rgb, sb, ns, h->maxval, st));
         HIP_TRY(hipStreamSynchronize(st));
-        comments = rep[0] != 0u;
-        s = (rep[1] ? 1u : 0u) | (rep[2] ? 2u : 0u);
+        // a token that is not a plain digit string (a comment, a '+' sign or an
+        // error): the general path redoes the body with the exact tokenizer
+        comments = rep[1] != 0u;
+        s = rep[2] ? 2u : 0u;
         n = (unsigned long long)rep[4] | ((unsigned long long)rep[5] << 32);
     }
     if (comments) {  // comments (or a body too short for the fast path): the general path
@@ -902,6 +908,7 @@ static int decode_ppm(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt
 extern "C" int dmmt_decode_ppm_device(dmmt_ctx* c, const uint8_t* d_text, size_t len, const dmmt_ppm_header* h,
                                       void* d_rgb, void* stream) {
     c = primary(c);
+    dmmt::error_detail(DMMT_OK, 0);
     if (!c || !h || (!d_text && len) || (!d_rgb && h->width && h->height)) return DMMT_E_INVALID_ARGUMENT;
     std::lock_guard<std::mutex> lk(c->mu);
     int rc;
@@ -1426,5 +1433,10 @@ extern "C" int dmmt_stripe_encode(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STRI
 }
 
 extern "C" const char* dmmt_build_info(void) {
-    return "dmmt-jpeg-encoder_amd: HIP kernels for gfx950, -ffp-contract=off, ABI " "1";
+#if DMMT_SDWA_PEEPHOLE
+#define DMMT_SDWA_NOTE "SDWA peephole on (measurement build)"
+#else
+#define DMMT_SDWA_NOTE "-mllvm -amdgpu-sdwa-peephole=false"
+#endif
+    return "dmmt-jpeg-encoder_amd: HIP kernels for gfx950, -ffp-contract=off, " DMMT_SDWA_NOTE ", ABI " "1";
 }

@@ -264,6 +264,48 @@ __device__ __forceinline__ void copy_slot(const uint32_t* __restrict__ sSlot, in
     }
 }
 
+// The same copy, unrolled and without a window clear (the product path): the
+// thread of block t (stream order: its offset is its own scan value, its walker
+// the rank it drew in the sort) reads all kSlotWords words of the walker's slot at
+// once -- no barrier is needed between the scan and the copy -- then
+//  copy_owned  (phase 1) stores, plainly, every window word whose first bit lies
+//              in its block: word d0 + k = {slot[k-1], slot[k]} >> sh (slot[-1] =
+//              0) for k >= 1, and k = 0 too when the block starts word-aligned --
+//              each window word has exactly one such block, so no word needs
+//              clearing and none is written twice;
+//  copy_head   (phase 2, after a barrier) ORs the block's first 32 - sh bits into
+//              word d0, which an earlier block owns (a word can collect the heads
+//              of several short blocks).
+// The looped version waited out one LDS read per copied word.
+struct SlotWords {
+    uint32_t w[kSlotWords];
+};
+__device__ __forceinline__ void read_slot(const uint32_t* __restrict__ sSlot, int tid, uint32_t nbits, SlotWords& W) {
+    const int nsw = (int)((nbits + 31) >> 5);
+#pragma unroll
+    for (int k = 0; k < kSlotWords; ++k) W.w[k] = sSlot[k * kEmitThreads + tid];
+#pragma unroll
+    for (int k = 0; k < kSlotWords; ++k) W.w[k] = k < nsw ? W.w[k] : 0u;  // words past the block: stale
+}
+__device__ __forceinline__ void copy_owned(const SlotWords& W, uint32_t s0, uint32_t nbits, uint32_t* sW, int w0,
+                                           int wn) {
+    if (!nbits) return;
+    const uint32_t sh = s0 & 31u;
+    const int d0 = (int)(s0 >> 5), d1 = (int)((s0 + nbits - 1) >> 5);
+#pragma unroll
+    for (int k = 0; k <= kSlotWords; ++k) {
+        const int d = d0 + k;
+        const uint32_t v = __builtin_amdgcn_alignbit(k ? W.w[k - 1] : 0u, k < kSlotWords ? W.w[k] : 0u, sh);
+        if (d <= d1 && (k || !sh) && (unsigned)(d - w0) <= (unsigned)wn) sW[d - w0] = v;
+    }
+}
+__device__ __forceinline__ void copy_head(const SlotWords& W, uint32_t s0, uint32_t nbits, uint32_t* sW, int w0,
+                                          int wn) {
+    const uint32_t sh = s0 & 31u;
+    const int d0 = (int)(s0 >> 5);
+    if (nbits && sh && (unsigned)(d0 - w0) <= (unsigned)wn) atomicOr(&sW[d0 - w0], W.w[0] >> sh);
+}
+
 // 16 bits of an MSB-first word stream starting at bit p (p & 31 taken; words a, b
 // hold bits from (p & ~31))
 __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
@@ -289,7 +331,9 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     __shared__ uint32_t sBin[65];  // walk order: blocks counted, then started, by last non-zero position
+#ifdef DMMT_EMIT_COPY_LOOP
     __shared__ uint32_t sStart[kEmitThreads];  // bit offset of block t in the chunk
+#endif
     using OrderT = std::conditional_t<(kEmitThreads > 256), uint16_t, uint8_t>;
     uint32_t* const sBits = sW;                                                      // bit count of block t
     OrderT* const sOrder = reinterpret_cast<OrderT*>(sW + kEmitThreads);               // block walked by thread u
@@ -303,14 +347,21 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     const int nb = span.nb;
     const long long e = (long long)frame * g.bpf + el0 + tid;
     const size_t cid = (size_t)frame * g.nch + chunk;
-    {  // code_tab: [luma DC][luma AC][chroma DC][chroma AC] x 256
-        const uint32_t* ct = code_tab + (size_t)frame * 1024;
-        if (tid < 256) {
-            sTab[tid] = ct[256 + tid];
-            sTab[256 + tid] = ct[768 + tid];
-        }
-        if (tid < 32) sTab[512 + tid] = ct[(tid < 16 ? 0 : 512 - 16) + tid];
+    // every global load of the prologue is issued before any is used (one latency,
+    // not three): the code tables -- code_tab is [luma DC][luma AC][chroma DC]
+    // [chroma AC] x 256; two AC words per thread, one DC word for threads below 32
+    // -- and the block's last non-zero position (at a clamped index past nb)
+    const bool valid = tid < nb;
+    const uint32_t* ct = code_tab + (size_t)frame * 1024;
+    const int tt = tid & 255;
+    const uint32_t tac0 = ct[256 + tt], tac1 = ct[768 + tt];
+    const uint32_t tdc = ct[((tt & 31) < 16 ? 0 : 512 - 16) + (tt & 31)];
+    const uint32_t lz = lastnz[valid ? e : (long long)frame * g.bpf + el0];
+    if (tid < 256) {
+        sTab[tid] = tac0;
+        sTab[256 + tid] = tac1;
     }
+    if (tid < 32) sTab[512 + tid] = tdc;
     if (chunk == 0) {  // the histogram replicas k_tables read: zero for the next launch
         for (int i = tid; i < kHistReps * 512; i += kEmitThreads) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
         for (int i = tid; i < kHistReps * 32; i += kEmitThreads) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
@@ -318,14 +369,13 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     if (tid < 8) sFF[tid] = 0u;
     if (tid < 3) sEdge[tid] = 0u;
     if (tid < 65) sBin[tid] = 0u;
-    const bool valid = tid < nb;
     // Walk order: a wave pays for every zigzag position at which any of its 64
     // blocks still has a non-zero coefficient, so the chunk's blocks are handed to
     // the threads sorted by their last non-zero position (k_front's lastnz): at
     // 4K q90 the mean over waves of the last such position falls from 61 to 39.
     // Thread u walks block sOrder[u] into its own slot u; after the scan (in
     // stream order) it shifts that slot into the window at the block's offset.
-    const int key = valid ? (int)lastnz[e] : 64;
+    const int key = valid ? (int)lz : 64;
     __syncthreads();
     const uint32_t rank = atomicAdd(&sBin[key], 1u);
     __syncthreads();
@@ -386,13 +436,29 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     }
     DMMT_TRACE(1);
 
+#ifdef DMMT_EMIT_COPY_LOOP
     sStart[tid] = start;  // (read by the block's walker after the window clear's barrier)
+#endif
     uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
     const int nw = (int)((total + 31) >> 5);
     const int we1 = total >= 16 ? (int)((total - 16) >> 5) : 0;  // word holding bit total-16
     uint32_t ff[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int w0 = 0; w0 < nw; w0 += kEmitWords) {  // uniform; one window unless the chunk is huge
         const int wn = min(kEmitWords, nw - w0);
+#ifndef DMMT_EMIT_COPY_LOOP
+        if (!over) {  // (uniform) block tid's bits from its walker's slot (column `mine`)
+            SlotWords sw;
+            read_slot(sSlot, mine, bits, sw);
+            if (tid == 0 && w0 + wn >= nw) sW[wn] = 0u;  // past the stream: no block owns it
+            copy_owned(sw, start, bits, sW, w0, wn);
+            __syncthreads();
+            copy_head(sw, start, bits, sW, w0, wn);
+        } else {
+            for (int i = tid; i <= wn; i += kEmitThreads) sW[i] = 0u;  // + the next window's first word
+            __syncthreads();
+        }
+        if (over && bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
+#else
         for (int i = tid; i <= wn; i += kEmitThreads) sW[i] = 0u;  // + the next window's first word
         __syncthreads();
         if (!over) {
@@ -400,6 +466,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             // are consecutive words)
             copy_slot(sSlot, tid, wbits ? sStart[pw] : 0u, wbits, sW, w0, wn);
         } else if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
+#endif
             {
                 // the block again (L2 / MALL) and a second walk straight into the
                 // window: holding it in registers across the scan would halve the

@@ -193,126 +193,86 @@ struct PpmText {
     long long nfast;      // comment-free chunks (kFastChunk bytes)
 };
 
-// Comment-free bodies (no '#' after the header: every P3 writer's output) take a
-// fast path in which a token starts at every token byte whose previous byte is
-// whitespace (or the body start), so a chunk's token count is a plain sum and its
-// first token's index a plain prefix sum.  The first launch also raises `flag` if
-// any '#' is present; the transition-map kernels then do the general work (and
-// are empty launches otherwise).
+// ---------------------------------------------------------------- comment-free path
+// Bodies whose tokens are all plain digit strings (every P3 writer's output) take
+// two passes over 16 KB chunks, the text loaded in coalesced 16-byte pieces
+// (piece p of a chunk = bytes [16p, 16p + 16); thread t holds pieces t, t + 256,
+// t + 512, t + 768):
+//  k_ppm_count   each chunk's token count: a token starts at every non-whitespace
+//                byte whose previous byte is whitespace (or lies before the body)
+//  k_ppm_rows    one workgroup: exclusive sums of the counts over 1024 rows of chunks
+//  k_ppm_fast    each chunk: the text staged in LDS, its token starts compacted in
+//                text order (a workgroup scan of the per-piece counts), then one
+//                thread per token -- its digits checked and combined with v_dot4
+//                (up to 8 digits; longer tokens are walked) -- and the sample stored
+//                at the chunk's first token index + the token's rank
+// The pass is optimistic: '#' is not whitespace, so a comment's first byte lies in
+// some token, and that token (like a '+' sign or any other non-digit) fails the
+// digit check and raises `bad`; the host then redoes the body on the general path,
+// which implements the tokenizer exactly (comments, signs, error precedence).
+// Bytes outside the body read as ' ' (they end tokens and start none).
 
-// 0x80 in every byte of y that is zero
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t y) {
-    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+// 0x80 in every byte of x that is not ASCII whitespace (char::is_ascii_whitespace:
+// ' ', \t, \n, \x0C, \r).  The whitespace bytes b are those with T[b & 7] == b & 0xF8
+// for the 8-entry table T = {0x20, 0x08, 0x08, -, 0x08, 0x08, -, -} (- = 0x01, which
+// no b & 0xF8 equals): one v_perm_b32 lookup, one xor3, a zero-byte test.
+__device__ __forceinline__ uint32_t sig_bytes(uint32_t x) {
+    const uint32_t idx = x & 0x07070707u;
+    const uint32_t tb = __builtin_amdgcn_perm(0x01010808u, 0x01080820u, idx);
+    const uint32_t y = tb ^ x ^ idx;  // zero exactly in the whitespace bytes
+    return (((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
 }
 
-// whitespace bytes of a word (char::is_ascii_whitespace), 4 bits: ' ' by a zero
-// test, 9 10 12 13 as the bytes in 8..15 whose low 3 bits select a 1 in an
-// 8-entry byte table (v_perm_b32)
-__device__ __forceinline__ uint32_t ws_hi(uint32_t x) {  // 0x80 in every whitespace byte
-    const uint32_t sp = zero_bytes(x ^ 0x20202020u);
-    const uint32_t in8 = zero_bytes((x & 0xF8F8F8F8u) ^ 0x08080808u);
-    const uint32_t lk = __builtin_amdgcn_perm(0x00000101u, 0x00010100u, x & 0x07070707u);
-    return sp | (in8 & (lk << 7));
-}
-__device__ __forceinline__ uint32_t ws4(uint32_t x) {  // the same as 4 bits (shifts: no quarter-rate multiply)
-    const uint32_t h = ws_hi(x);
-    return ((h >> 7) & 1u) | ((h >> 14) & 2u) | ((h >> 21) & 4u) | (h >> 28);
+// 0x80 in every byte of x that is not an ASCII digit
+__device__ __forceinline__ uint32_t nondigit_bytes(uint32_t x) {
+    const uint32_t ge30 = (x | 0x80808080u) - 0x30303030u;  // bit 7: (b & 0x7F) >= '0'
+    const uint32_t ge3a = (x & 0x7F7F7F7Fu) + 0x46464646u;  // bit 7: (b & 0x7F) > '9'
+    return (~ge30 | ge3a | x) & 0x80808080u;
 }
 
-// A thread's 64 bytes for the comment-free path: its words, valid bytes and
-// whitespace (bit i = byte i), and whether it holds a '#'.  Lane 0 also reads the
-// byte before the window and lane 63 the 4 bytes after it (their neighbours'
-// windows are in other waves).  All loads are unconditional, at clamped addresses
-// inside the caller's buffer (the launcher guarantees t.len - t.safe >= 96), so
-// they are in flight together; windows at the ends of the body are fixed up
-// byte-wise.
-struct FastWin {
-    uint32_t w[16];
-    unsigned long long valid, ws;
-    bool hash;
-    uint32_t prev_sig;  // lane 0: the byte before the window is a token byte
-    uint32_t next_w;    // lane 63: the 4 bytes after the window (0 past the text)
-    uint32_t next_end;  // lane 63: which of them end a token (whitespace, past the text)
-};
-
-__device__ __forceinline__ void fast_window(const PpmText& t, long long pos, FastWin& F, bool want_next) {
-    const int lane = lane_id();
+// A thread's four pieces of the chunk at c0 (piece q at c0 + 16 (tid + 256 q)):
+// issue_pieces issues the four loads together at clamped in-buffer addresses (the
+// launcher guarantees t.len - t.safe >= 96); fix_pieces then rebuilds a piece that
+// crosses an end of the body byte by byte: bytes outside [lo, len) read as ' ' and
+// are never fetched.
+__device__ __forceinline__ void issue_pieces(const PpmText& t, long long c0, int tid, uint4 (&v)[4], bool (&full)[4]) {
     const long long s16 = (t.safe + 15) & ~15ll;
-    const bool full = pos >= t.safe && pos + kFastWin <= t.len;
-    const uint4* src = reinterpret_cast<const uint4*>(t.text + (full ? pos : s16));
-    uint4 v[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = src[q];
-    const uint32_t pb = t.text[min(max(pos - 1, t.lo), t.len - 1)];
-    const long long qn = pos + kFastWin;
-    const uint32_t nw = want_next ? *reinterpret_cast<const uint32_t*>(t.text + min(qn, (t.len - 4) & ~3ll)) : 0u;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        F.w[4 * q] = full ? v[q].x : 0u;
-        F.w[4 * q + 1] = full ? v[q].y : 0u;
-        F.w[4 * q + 2] = full ? v[q].z : 0u;
-        F.w[4 * q + 3] = full ? v[q].w : 0u;
+        const long long pos = c0 + 16 * (tid + kPpmThreads * q);
+        full[q] = pos >= t.lo && pos + 16 <= t.len;
+        v[q] = *reinterpret_cast<const uint4*>(t.text + (full[q] ? pos : s16));
     }
-    F.prev_sig = (lane == 0 && pos - 1 >= t.lo && pos - 1 < t.len) ? (uint32_t)!ppm_ws(pb) : 0u;
-    F.next_w = 0u;
-    F.next_end = 0xFu;
-    if (want_next && lane == 63) {
-        if (qn + 4 <= t.len) {
-            F.next_w = nw;
-            F.next_end = ws4(nw);
-        } else {
-            for (int j = 0; j < 4; ++j)
-                if (qn + j < t.len) F.next_w |= (uint32_t)t.text[qn + j] << (8 * j);
-            const long long in = qn < t.len ? t.len - qn : 0;  // bytes of the 4 inside the text
-            F.next_end = (ws4(F.next_w) | ~((1u << (int)in) - 1u)) & 0xFu;
+}
+__device__ __forceinline__ void fix_pieces(const PpmText& t, long long c0, int tid, const uint4 (&v)[4],
+                                           const bool (&full)[4], uint32_t (&w)[4][4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        w[q][0] = v[q].x, w[q][1] = v[q].y, w[q][2] = v[q].z, w[q][3] = v[q].w;
+        if (!full[q]) {
+            const long long pos = c0 + 16 * (tid + kPpmThreads * q);
+            for (int k = 0; k < 4; ++k) w[q][k] = 0x20202020u;
+            for (int k = 0; k < 16; ++k)
+                if (pos + k >= t.lo && pos + k < t.len)
+                    w[q][k >> 2] = (w[q][k >> 2] & ~(0xFFu << (8 * (k & 3)))) | ((uint32_t)t.text[pos + k] << (8 * (k & 3)));
         }
     }
-    F.valid = F.ws = 0ull;
-    F.hash = false;
-    if (pos + kFastWin <= t.lo || pos >= t.len) return;
-    if (!full) {
-        for (int k = 0; k < kFastWin; ++k)
-            if (pos + k >= t.lo && pos + k < t.len) F.w[k >> 2] |= (uint32_t)t.text[pos + k] << (8 * (k & 3));
-    }
-    const long long a = t.lo > pos ? t.lo - pos : 0, b = t.len - pos < kFastWin ? t.len - pos : kFastWin;
-    F.valid = (b == 64 ? ~0ull : (1ull << (int)b) - 1ull) & ~((1ull << (int)a) - 1ull);
-    unsigned long long ws = 0;
-    uint32_t hz = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        ws |= (unsigned long long)ws4(F.w[k]) << (4 * k);
-        hz |= zero_bytes(F.w[k] ^ 0x23232323u);
-    }
-    F.ws = ws & F.valid;
-    F.hash = hz != 0u;  // (bytes outside the text are 0, never '#')
 }
 
-// the window's token starts when there are no comments: the previous byte is
-// the previous thread's last (a shuffle) or, for lane 0, read back
-__device__ __forceinline__ unsigned long long fast_starts(const FastWin& W) {
-    const unsigned long long sig = W.valid & ~W.ws;
-    uint32_t prev = lane_prev_u32((uint32_t)(sig >> 63));  // (the wave is whole here)
-    if (lane_id() == 0) prev = W.prev_sig;
-    return sig & ~((sig << 1) | prev);
+// the byte at pos (clamped into the buffer, loaded unconditionally) and, once it
+// has arrived, whether it is a body token byte (0 outside the body)
+__device__ __forceinline__ uint32_t load_byte_clamped(const PpmText& t, long long pos) {
+    return t.text[min(max(pos, t.safe), t.len - 1)];
+}
+__device__ __forceinline__ uint32_t body_sig(const PpmText& t, long long pos, uint32_t b) {
+    return pos >= t.lo && pos < t.len ? (uint32_t)!ppm_ws(b) : 0u;
 }
 
-// ---------------------------------------------------------------- comment-free path
-// Bodies without '#' (every P3 writer's output) in two passes over the text,
-// 16 KB chunks (64 bytes per thread):
-//  k_ppm_count   each chunk's token count (a token starts at every token byte
-//                after whitespace); raises `flag` on any '#'
-//  k_ppm_carry   one workgroup: exclusive sums of the counts over 1024 rows of
-//                chunks (or, with comments, the transition-map scan of the
-//                general path)
-//  k_ppm_fast    each chunk: its row's base plus the counts before it in the row,
-//                then its tokens parsed token by token (every lane busy until the
-//                wave's largest count; the window's words from LDS) -- a token of
-//                at most 4 bytes is one byte-align of two words, its digits
-//                checked and combined per byte lane (SWAR); longer ones, '+' and
-//                bad tokens take the byte walk -- staged in LDS in token order at
-//                the output's alignment and stored as aligned 16-byte pieces
-// With a '#' anywhere these write nothing that is used: the general kernels
-// (k_ppm_maps, k_ppm_parse) redo the body.
+// token starts of one word (0x80 per start byte) given the previous word's
+// non-whitespace bytes (only its top byte matters)
+__device__ __forceinline__ uint32_t starts_of(uint32_t sig, uint32_t prev) {
+    return sig & ~__builtin_amdgcn_alignbyte(sig, prev, 3u);
+}
 
 // A token from byte p (a token start) to the next kept whitespace, as
 // `str::parse::<u16>` (ppm.rs:247-251): the general byte walk, comments included.
@@ -372,39 +332,61 @@ struct PpmReport {
     unsigned long long tokens;
 };
 
-__global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* __restrict__ counts,
-                                                           PpmReport* __restrict__ rep) {
-    __shared__ uint32_t sRed[kPpmThreads / 64];
-    const int tid = threadIdx.x;
-    const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
-    FastWin F;
-    fast_window(t, pos, F, false);
-    const uint32_t n = wave_sum_full_u32((uint32_t)__popcll(fast_starts(F)));
-    if (lane_id() == 0) sRed[tid >> 6] = n;
-    const bool hash = __syncthreads_or(F.hash) != 0;
-    if (tid == 0) {
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t sRed[kPpmThreads / 64], sF[kPpmThreads / 64], sL[kPpmThreads / 64];
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const long long c0 = (long long)blockIdx.x * kFastChunk;
+    uint4 v[4];
+    bool full[4];
+    issue_pieces(t, c0, tid, v, full);
+    const uint32_t bb = load_byte_clamped(t, c0 - 1);  // the byte before the chunk
+    uint32_t w[4][4];
+    fix_pieces(t, c0, tid, v, full, w);
+    const uint32_t before = body_sig(t, c0 - 1, bb);  // a token running in from the previous chunk
+    // starts of each piece as if the byte before it were whitespace; fb / lb: whether
+    // piece q's first / last byte is a token byte
+    uint32_t n = 0, fb = 0, lb = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t prev = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t s = sig_bytes(w[q][k]);
+            n += (uint32_t)__popc(starts_of(s, prev));
+            prev = s;
+            if (k == 0) fb |= ((s >> 7) & 1u) << q;
+            if (k == 3) lb |= (s >> 31) << q;
+        }
+    }
+    // piece (q, lane) follows piece (q, lane - 1): a token across the seam counted twice
+    n -= (uint32_t)__popc(fb & lane_prev_u32(lb));  // (lane 0: 0)
+    n = wave_sum_full_u32(n);
+    if (lane == 0) {
+        sRed[wave] = n;
+        sF[wave] = fb;
+    }
+    if (lane == 63) sL[wave] = lb;
+    __syncthreads();
+    if (tid == 0) {  // the seams at each wave's lane 0: piece (q, 64 w - 1), or (q - 1, 255)
         uint32_t c = 0;
-        for (int q = 0; q < kPpmThreads / 64; ++q) c += sRed[q];
+#pragma unroll
+        for (int v = 0; v < kPpmThreads / 64; ++v) {
+            c += sRed[v];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t pb = v ? (sL[v - 1] >> q) & 1u : (q ? (sL[kPpmThreads / 64 - 1] >> (q - 1)) & 1u : before);
+                c -= (sF[v] >> q) & pb & 1u;
+            }
+        }
         counts[blockIdx.x] = c;
-        if (hash) reinterpret_cast<volatile uint32_t*>(&rep->comment)[0] = 1u;
     }
 }
 
-// The token starting at byte i = 4j + r of a thread's window (lo, hi: words j
-// and j+1; e8: which of bytes 4j .. 4j+7 end a token): at most 4 digits by SWAR
-// -- one byte-align, digits checked per byte lane and combined with 24-bit
-// multiplies -- else ok = false and the caller walks it.
-__device__ __forceinline__ uint32_t fast_token(int r, uint32_t lo, uint32_t hi, uint32_t e8, bool& ok) {
-    const uint32_t e = (e8 >> r) & 0x1Fu;
-    const uint32_t L = e ? (uint32_t)__builtin_ctz(e) : 5u;
-    const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)r);
-    const uint32_t m = L >= 4 ? 0xFFFFFFFFu : (1u << (8 * L)) - 1u;
-    const uint32_t ge30 = ((x | 0x80808080u) - 0x30303030u) & 0x80808080u;
-    const uint32_t ge3a = ((x & 0x7F7F7F7Fu) + 0x46464646u) & 0x80808080u;
-    ok = L <= 4 && (((~ge30 | ge3a | x) & 0x80808080u) & m) == 0u;
-    const uint32_t d = (x & 0x0F0F0F0Fu & m) << (8 * (4 - min(L, 4u)));  // leading zero digits
-    const uint32_t t1 = __umul24(d & 0x00FF00FFu, 10u) + ((d >> 8) & 0x00FF00FFu);
-    return __umul24(t1 & 0xFFFFu, 100u) + (t1 >> 16);
+// digits in the low nibbles of the bytes of d, the last one in byte 3 (leading
+// bytes zero) -> their decimal value
+__device__ __forceinline__ uint32_t digits4(uint32_t d) {
+    const uint32_t a = __builtin_amdgcn_udot4(d, 0x00010A64u, 0u, false);  // 100 b0 + 10 b1 + b2
+    return __umul24(a, 10u) + (d >> 24);
 }
 
 template <typename Out>
@@ -413,85 +395,183 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                                                           const unsigned long long* __restrict__ row_base,
                                                           long long per, Out* __restrict__ out,
                                                           unsigned long long nsamples, uint32_t maxval) {
-    __shared__ uint32_t sWave[kPpmThreads / 64];
+    constexpr int NW = kPpmThreads / 64;
+    __shared__ uint32_t sText[kFastChunk / 4 + 4];  // the chunk (' ' outside the body) + the next 16 bytes
+    __shared__ uint16_t sIdx[kFastChunk / 2];      // token starts (chunk offsets) in text order
+    __shared__ uint32_t sScan[NW][2];
     __shared__ unsigned long long sBase;
-    // at most one token per two bytes, staged at the output's 16-byte alignment
-    __shared__ __attribute__((aligned(16))) Out sOut[kFastChunk / 2 + 16 / sizeof(Out)];
-    __shared__ uint32_t sWin[kPpmThreads * 17];  // each lane's 16 window words + the next one
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const long long pos = (long long)blockIdx.x * kFastChunk + (long long)tid * kFastWin;
-    // the first token's index: the row's base + the counts before this chunk in
-    // its row (wave 0; loads issued beside the window's)
+    const long long c0 = (long long)blockIdx.x * kFastChunk;
     const long long row0 = (long long)(blockIdx.x / per) * per, bx = (long long)blockIdx.x;
-    FastWin F;
-    fast_window(t, pos, F, true);
-    const uint32_t c0 = counts[min(row0 + lane, bx)];
-    uint32_t cnt = row0 + lane < bx ? c0 : 0u;
-    for (long long r0 = row0 + 64; r0 < bx; r0 += 64) {  // rows of more than 64 chunks (texts > 1 GB)
-        const uint32_t c = counts[min(r0 + lane, bx)];
-        cnt += r0 + lane < bx ? c : 0u;
+    // every load of the prologue is issued before any is used: the pieces, the next
+    // chunk's first 16 bytes (a word for each of threads 0-3), the byte before the
+    // chunk, and for the first token's index the row's base + the counts before this
+    // chunk in its row (wave 0)
+    uint4 v[4];
+    bool full[4];
+    issue_pieces(t, c0, tid, v, full);
+    const long long tp = c0 + kFastChunk + 4 * (tid & 3);
+    const bool tfull = tp >= t.lo && tp + 4 <= t.len;
+    uint32_t tw = *reinterpret_cast<const uint32_t*>(t.text + (tfull ? tp : (t.safe + 15) & ~15ll));
+    const uint32_t bb = load_byte_clamped(t, c0 - 1);
+    const uint32_t cfirst = counts[min(row0 + lane, bx)];
+    const unsigned long long rbase = row_base[blockIdx.x / per];
+    uint32_t cnt = row0 + lane < bx ? cfirst : 0u;
+    if (wave == 0) {
+        for (long long r0 = row0 + 64; r0 < bx; r0 += 64) {  // rows of more than 64 chunks (texts > 1 GB)
+            const uint32_t c = counts[min(r0 + lane, bx)];
+            cnt += r0 + lane < bx ? c : 0u;
+        }
     }
-    const unsigned long long starts = fast_starts(F);
-    const uint32_t n = (uint32_t)__popcll(starts);
-    const unsigned long long ends = F.ws | ~F.valid;  // bytes that end a token
-    uint32_t wn = lane_next_u32(F.w[0]);
-    uint32_t next4 = lane_next_u32((uint32_t)(ends & 0xFull)) & 0xFu;
-    if (lane == 63) {  // the next window belongs to the next wave (or chunk)
-        wn = F.next_w;
-        next4 = F.next_end;
+    uint32_t w[4][4];
+    fix_pieces(t, c0, tid, v, full, w);
+    const uint32_t before = body_sig(t, c0 - 1, bb);
+    if (!tfull) {
+        tw = 0x20202020u;
+        for (int j = 0; j < 4; ++j)
+            if (tp + j >= t.lo && tp + j < t.len) tw = (tw & ~(0xFFu << (8 * j))) | ((uint32_t)t.text[tp + j] << (8 * j));
     }
-    const uint32_t inc = wave_incl_scan_full_u32(n);
-    if (lane == 63) sWave[wave] = inc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        reinterpret_cast<uint4*>(sText)[tid + kPpmThreads * q] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
+    if (tid < 4) sText[kFastChunk / 4 + tid] = tw;
+    __syncthreads();
+    // token starts per word; a piece's previous byte is the last of piece (q, t - 1):
+    // a lane shuffle, or for a wave's lane 0 the staged byte (the byte before the
+    // chunk for piece 0)
+    uint32_t st[4][4];
+    uint32_t n01 = 0, n23 = 0;  // starts per piece, two 16-bit fields each
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t s[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] = sig_bytes(w[q][k]);
+        uint32_t prev = lane_prev_u32(s[3]);
+        if (lane == 0) {
+            const int p = tid + kPpmThreads * q;
+            const uint32_t pb = p ? (uint32_t)!ppm_ws((sText[(4 * p - 1)] >> 24)) : before;
+            prev = pb << 31;
+        }
+        uint32_t nq = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            st[q][k] = starts_of(s[k], prev);
+            prev = s[k];
+            nq += (uint32_t)__popc(st[q][k]);
+        }
+        if (q < 2)
+            n01 |= nq << (16 * q);
+        else
+            n23 |= nq << (16 * (q - 2));
+    }
+    const uint32_t i01 = wave_incl_scan_full_u32(n01), i23 = wave_incl_scan_full_u32(n23);
+    if (lane == 63) {
+        sScan[wave][0] = i01;
+        sScan[wave][1] = i23;
+    }
     if (wave == 0) {
         cnt = wave_sum_full_u32(cnt);
-        if (lane == 0) sBase = row_base[blockIdx.x / per] + cnt;
+        if (lane == 0) sBase = rbase + cnt;
     }
     __syncthreads();
-    uint32_t slot = inc - n, total = 0;
-    for (int q = 0; q < kPpmThreads / 64; ++q) {
-        slot += q < wave ? sWave[q] : 0u;
-        total += sWave[q];
-    }
-    uint32_t bad = 0, over = 0;
-    const unsigned long long base = sBase;
-    const uint32_t delta = (uint32_t)((reinterpret_cast<uintptr_t>(out + base) & 15u) / sizeof(Out));
-    slot += delta;
-    uint32_t* const win = sWin + tid * 17;
+    uint32_t e01 = i01 - n01, e23 = i23 - n23, t01 = 0, t23 = 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) win[q] = F.w[q];
-    win[16] = wn;
-    unsigned long long st = starts;
-    while (__any(st != 0ull)) {  // token by token: every lane busy until the wave's largest count
-        if (st) {
-            const int r = __builtin_ctzll(st);
-            st &= st - 1ull;
-            const int j = r >> 2;
-            const uint32_t lo = win[j], hi = win[j + 1];
-            const uint32_t e8 = j < 15 ? (uint32_t)(ends >> (4 * j)) & 0xFFu
-                                       : ((uint32_t)(ends >> 60) & 0xFu) | (next4 << 4);
-            bool ok;
-            uint32_t v = fast_token(r & 3, lo, hi, e8, ok);
-            if (!ok) v = parse_token_walk(t, nullptr, 0, pos + r, ok);  // '+', long, not a number
-            bad |= !ok;
-            over |= ok && v > maxval;
-            sOut[slot++] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+    for (int v = 0; v < NW; ++v) {
+        e01 += v < wave ? sScan[v][0] : 0u;
+        e23 += v < wave ? sScan[v][1] : 0u;
+        t01 += sScan[v][0];
+        t23 += sScan[v][1];
+    }
+    const uint32_t T0 = t01 & 0xFFFFu, T1 = t01 >> 16, T2 = t23 & 0xFFFFu, T3 = t23 >> 16;
+    const uint32_t ntok = T0 + T1 + T2 + T3;
+    uint32_t rank[4] = {e01 & 0xFFFFu, T0 + (e01 >> 16), T0 + T1 + (e23 & 0xFFFFu), T0 + T1 + T2 + (e23 >> 16)};
+#if DMMT_PPM_ABL == 1  // study: the time up to the compaction
+    if (ntok == 12345678u) rep->bad = 1u;
+    return;
+#endif
+    // compaction: at most two starts per word (a start follows whitespace)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t off = 16u * (uint32_t)(tid + kPpmThreads * q);
+        uint32_t r = rank[q];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t m = st[q][k];
+            if (m) {
+                sIdx[r] = (uint16_t)(off + 4 * k + (__builtin_ctz(m) >> 3));
+                const uint32_t last = (uint32_t)(31 - __clz((int)m)) >> 3;
+                if (m & (m - 1u)) sIdx[r + 1] = (uint16_t)(off + 4 * k + last);
+                r += (uint32_t)__popc(m);
+            }
         }
     }
     __syncthreads();
-    const unsigned long long lim = base < nsamples ? min((unsigned long long)total, nsamples - base) : 0ull;
-    // aligned 16-byte pieces; the first and last piece only where they hold this
-    // chunk's samples
-    constexpr uint32_t S = sizeof(Out);
-    const uint32_t b_lo = delta * S, b_hi = (delta + (uint32_t)lim) * S;
-    uint8_t* const oa = reinterpret_cast<uint8_t*>(out + base) - b_lo;
-    const uint8_t* const so = reinterpret_cast<const uint8_t*>(sOut);
-    for (uint32_t b0 = 16u * (uint32_t)tid; b0 < b_hi; b0 += 16u * kPpmThreads) {
-        if (b0 >= b_lo && b0 + 16u <= b_hi) {
-            *reinterpret_cast<uint4*>(oa + b0) = *reinterpret_cast<const uint4*>(so + b0);
-        } else {
-            for (uint32_t i = max(b0, b_lo); i < min(b0 + 16u, b_hi); i += S)
-                *reinterpret_cast<Out*>(oa + i) = *reinterpret_cast<const Out*>(so + i);
+#if DMMT_PPM_ABL == 2  // study: the time up to the token loop
+    if (sIdx[tid] == 12345u) rep->bad = 1u;
+    return;
+#endif
+    // one thread per token, two tokens (i, i + 256) per iteration so that their
+    // LDS reads overlap; the common case (at most 4 digits) is branch-free, and the
+    // loop makes no global loads (a token of 9 or more digits is only marked here
+    // and walked afterwards), so its stores are never waited for inside it
+    const unsigned long long base = sBase;
+    uint32_t bad = 0, over = 0, longm = 0;
+    // a token's value from the chunk words at its start: v, whether it parsed, or
+    // (long) 9+ digits to walk
+    auto token = [&](uint32_t s, uint32_t lo, uint32_t hi, uint32_t& v, bool& ok, bool& lng) {
+        const uint32_t j = s >> 2, r = s & 3u;
+        const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, r);  // token bytes 0-3
+        const uint32_t nd = nondigit_bytes(x);
+        const uint32_t L = nd ? (uint32_t)__builtin_ctz(nd) >> 3 : 4u;  // leading digits (of these 4)
+        const uint32_t b4 = __builtin_amdgcn_ubfe(hi, 8 * r, 8);       // token byte 4
+        uint32_t tb = L < 4 ? __builtin_amdgcn_ubfe(x, (8 * L) & 31, 8) : b4;  // the byte after the digits
+        v = digits4((x & 0x0F0F0F0Fu) << ((32 - 8 * L) & 31));
+        lng = false;
+        if (L == 4 && tb - 0x30u < 10u) {  // 5 or more digits: bytes 4-7 (u16 samples)
+            const uint32_t h2 = sText[j + 2];
+            const uint32_t y = __builtin_amdgcn_alignbyte(h2, hi, r);
+            const uint32_t nd2 = nondigit_bytes(y);
+            const uint32_t L2 = nd2 ? (uint32_t)__builtin_ctz(nd2) >> 3 : 4u;  // >= 1
+            tb = L2 < 4 ? __builtin_amdgcn_ubfe(y, (8 * L2) & 31, 8) : __builtin_amdgcn_ubfe(h2, 8 * r, 8);
+            const uint32_t p10 = L2 == 1 ? 10u : L2 == 2 ? 100u : L2 == 3 ? 1000u : 10000u;
+            v = v * p10 + digits4((y & 0x0F0F0F0Fu) << ((32 - 8 * L2) & 31));
+            lng = L2 == 4 && tb - 0x30u < 10u;  // 9 or more
         }
+        // char::is_ascii_whitespace(tb): ' ', or one of \t \n \x0C \r (bits 9, 10, 12, 13)
+        const bool ws = tb == 0x20u || (tb < 14u && ((0x3600u >> tb) & 1u));
+        ok = L > 0 && ws && v <= 65535u;
+    };
+    uint32_t i = (uint32_t)tid;
+    for (int m = 0; i < ntok; i += 2 * kPpmThreads, m += 2) {
+        const uint32_t i1 = i + kPpmThreads;
+        const bool has1 = i1 < ntok;
+        const uint32_t s0 = sIdx[i], s1 = sIdx[has1 ? i1 : i];
+        const uint32_t lo0 = sText[s0 >> 2], hi0 = sText[(s0 >> 2) + 1];
+        const uint32_t lo1 = sText[s1 >> 2], hi1 = sText[(s1 >> 2) + 1];
+        uint32_t v0, v1;
+        bool ok0, ok1, lg0, lg1;
+        token(s0, lo0, hi0, v0, ok0, lg0);
+        token(s1, lo1, hi1, v1, ok1, lg1);
+        longm |= (lg0 ? 1u << m : 0u) | (has1 && lg1 ? 2u << m : 0u);
+        lg1 = lg1 || !has1;
+        bad |= (!ok0 && !lg0) || (!ok1 && !lg1);
+        over |= (ok0 && !lg0 && v0 > maxval) || (ok1 && !lg1 && v1 > maxval);
+#if DMMT_PPM_ABL == 3  // study: the token loop without its stores
+        if (v0 + v1 == 0x12345u) out[0] = 1;
+#else
+        if (!lg0 && base + i < nsamples) out[base + i] = (Out)(sizeof(Out) == 1 ? min(v0, 255u) : min(v0, 65535u));
+        if (!lg1 && base + i1 < nsamples) out[base + i1] = (Out)(sizeof(Out) == 1 ? min(v1, 255u) : min(v1, 65535u));
+#endif
+    }
+    while (longm) {  // (rare) tokens of 9 or more digits: leading zeros, or a parse error
+        const int m = __builtin_ctz(longm);
+        longm &= longm - 1u;
+        const uint32_t k = (uint32_t)tid + kPpmThreads * (uint32_t)m;
+        bool ok;
+        const uint32_t v = parse_token_walk(t, nullptr, 0, c0 + sIdx[k], ok);
+        bad |= !ok;
+        over |= ok && v > maxval;
+        if (base + k < nsamples) out[base + k] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
     }
     if (bad) reinterpret_cast<volatile uint32_t*>(&rep->bad)[0] = 1u;
     if (over) reinterpret_cast<volatile uint32_t*>(&rep->over)[0] = 1u;
@@ -707,7 +787,7 @@ hipError_t launch_ppm_p3_fast(const uint8_t* text, size_t body_offset, size_t le
     PpmReport* r = reinterpret_cast<PpmReport*>(report);
     const unsigned nfast = (unsigned)t.nfast;
     const long long rper = ppm_row_chunks(t.nfast);
-    hipLaunchKernelGGL(k_ppm_count, dim3(nfast), dim3(kPpmThreads), 0, st, t, counts, r);
+    hipLaunchKernelGGL(k_ppm_count, dim3(nfast), dim3(kPpmThreads), 0, st, t, counts);
     hipLaunchKernelGGL(k_ppm_rows, dim3(1), dim3(kPpmCarryThreads), 0, st, (const uint32_t*)counts, t.nfast, rper, r,
                        row_base);
     if (sample_bytes == 1)

@@ -358,6 +358,15 @@ class Encoder:
         """member context i's handle (borrowed: valid while this context lives)"""
         return lib().dmmt_ctx_member(self._ctx, int(i)) or 0
 
+    def member_encoder(self, i: int) -> "Encoder":
+        """member context i as an Encoder view (device memory, synthetic frames,
+        copies on that member's device); borrowed: valid while this context lives,
+        and its close() leaves the member alone"""
+        h = self.member(i)
+        if not h:
+            raise Error(-102, f"no member {i}")  # DMMT_E_INVALID_ARGUMENT
+        return _MemberView(h, self.device if self.num_devices() == 1 else None)
+
     def encode_striped(self, image: "Image", options: "JpegTransformationOptions", n_stripes: int = 0) -> bytes:
         """one image as MCU-row stripes over the members (dmmt_jpeg_encode_striped)"""
         im = image.to_c()
@@ -714,6 +723,17 @@ def device_count() -> int:
     lib().dmmt_device_count(ctypes.byref(n))
     return n.value
 
+
+
+class _MemberView(Encoder):
+    """a borrowed member context of a multi-GPU Encoder (Encoder.member_encoder)"""
+
+    def __init__(self, handle: int, device=None):
+        self._ctx = ctypes.c_void_p(handle)
+        self.device = device
+
+    def close(self):
+        pass
 
 class AraiDiscrete8x8CosineTransformer:
     """The reference's pluggable DCT operator (cosine_transform.rs:13-73, arai.rs:95-104), on the GPU."""

@@ -219,7 +219,13 @@ int dmmt_stripe_write(dmmt_ctx* ctx, uint64_t bit_offset, uint32_t next_bits, ui
  *   dmmt_ctx_synchronize / _set_lanes / _set_profiling / _profile   every member
  *   any other call (device memory, stage-level, stripe_* steps)      member 0
  * Device-resident work names the member explicitly (dmmt_encode_device_multi,
- * dmmt_encode_striped_device) or goes to a member context (dmmt_ctx_member). */
+ * dmmt_encode_striped_device) or goes to a member context (dmmt_ctx_member).
+ * Each call locks the contexts it uses for its own duration, but a stripe_* sequence
+ * (analyze, measure, write) spans several calls: a group context -- and its members -- must not
+ * run a stripe_* sequence on one thread while another thread runs a group encode on it (the
+ * group's striped encodes use the members' stripe state).  Give concurrent work its own context.
+ * Operation across distinct physical GPUs is built the same way but has only been tested with
+ * repeated device ids on one GPU (no multi-GPU host was available). */
 #define DMMT_MAX_GROUP 64
 int dmmt_ctx_create_multi(const int* device_ids, int n, dmmt_ctx** out);
 int dmmt_ctx_num_devices(const dmmt_ctx* ctx);       /* members (1 for dmmt_ctx_create contexts) */

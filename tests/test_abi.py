@@ -58,6 +58,24 @@ def test_quality_tables(L, presets):
         dmmt_jpeg.quality_tables(0)
 
 
+def test_quality_tables_match_libjpeg(L):
+    """dmmt_quality_tables(q) (the IJG quality extension) against an
+    independent implementation: libjpeg's jpeg_set_quality(q, force_baseline)
+    through Pillow, whose decoded DQT tables come back in natural order, for every
+    q = 1..100.  The reference has no quality factor; q50 is its Specification
+    preset (quantization_tables.rs:286-327), checked in test_quality_tables."""
+    Image = pytest.importorskip("PIL.Image")
+    import io
+    im = Image.fromarray(np.zeros((8, 8, 3), np.uint8))
+    for q in range(1, 101):
+        buf = io.BytesIO()
+        im.save(buf, "JPEG", quality=q)
+        t = Image.open(io.BytesIO(buf.getvalue())).quantization
+        luma, chroma = dmmt_jpeg.quality_tables(q)
+        assert list(t[0]) == list(luma), q
+        assert list(t[1]) == list(chroma), q
+
+
 def test_default_options(L):
     o = dmmt_jpeg.DmmtOptions()
     L.dmmt_default_options(ctypes.byref(o))
@@ -244,3 +262,10 @@ def test_ppm_error_payload_token_names(L, text, code, token):
     with pytest.raises(dmmt_jpeg.Error) as e:
         dmmt_jpeg.PPMImageReader(text).read_image()
     assert e.value.code == code and f"'{token}'" in str(e.value)
+
+
+def test_build_info_reports_no_sdwa_peephole(L):
+    """every device object is built without the SDWA peephole (the round-3/4 study:
+    profiles/r03_kemit_fault_study.md); the library says so"""
+    info = L.dmmt_build_info().decode()
+    assert "-amdgpu-sdwa-peephole=false" in info and "gfx950" in info

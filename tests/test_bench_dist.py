@@ -165,3 +165,64 @@ def test_bench_refuses_world_mismatch(monkeypatch):
     with pytest.raises(SystemExit):
         bench.main(["--gpus", "4", "--steps", "1", "--warmup", "0", "--cpu-seconds", "0", "--ppm-steps", "0"],
                    make_encoder=lambda lr: StandInEncoder(lr, 0, []), emit=lambda l: None)
+
+
+class StandInGroup:
+    """a multi-device context stand-in: members record their frames, the group
+    records each enqueue (one batch of frames per member per call)"""
+
+    def __init__(self, ids, log):
+        self.ids, self.log = list(ids), log
+        self.members = [StandInEncoder(0, i, log) for i in range(len(ids))]
+
+    def num_devices(self):
+        return len(self.ids)
+
+    def member_encoder(self, i):
+        return self.members[i]
+
+    def set_lanes(self, n):
+        self.log.append(("group_lanes", n))
+
+    def encode_device_multi(self, frames, opts):
+        assert len(frames) == len(self.ids)
+        self.log.append(("multi", tuple(int(f.d_rgb) for f in frames), tuple(int(f.n_frames) for f in frames)))
+        time.sleep(0.001)
+
+    def synchronize(self):
+        self.log.append(("sync",))
+
+    def close(self):
+        self.log.append(("close",))
+
+
+def test_bench_inproc_group(monkeypatch):
+    """`bench.py --gpus 4 --inproc`: one process, the C ABI's multi-GPU context
+    (dmmt_ctx_create_multi); each step is one dmmt_encode_device_multi call with
+    one batch per member, every member encoding its own distinct frames; value =
+    all members' pixels / elapsed, weak scaling.  Repeated ids (--devices 0,0)
+    rehearse it on one GPU."""
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    import bench
+    for argv, ids in ((["--gpus", "4"], [0, 1, 2, 3]), (["--gpus", "1", "--devices", "0,0"], [0, 0])):
+        log, lines, made = [], [], []
+
+        def make_group(i, log=log, made=made):
+            made.append(list(i))
+            return StandInGroup(i, log)
+        bench.main(argv + ["--inproc", "--steps", "6", "--warmup", "2", "--cpu-seconds", "0", "--ppm-steps", "0"],
+                   make_group=make_group, emit=lines.append)
+        assert made == [ids] and len(lines) == 1
+        line = json.loads(lines[0])
+        n = len(ids)
+        assert line["n_gpus"] == len(set(ids)) and line["scaling"] == "weak" and line["config"]["members"] == n
+        assert line["config"]["device_ids"] == ids
+        calls = [x for x in log if x[0] == "multi"]
+        assert len(calls) == 8  # warmup + steps, one call per step
+        # distinct synthetic frames for every member
+        firsts = [x[2] for x in log if x[0] == "frames"]
+        assert len(firsts) == len(set(firsts)) == n * line["config"]["input_slots_per_member"]
+        expect = n * 3840 * 2160 * 6 / (line["ms_per_step"] * 6 / 1e3) / 1e6
+        assert line["value"] == pytest.approx(expect, rel=2e-3)
+        assert log[-1] == ("close",)
