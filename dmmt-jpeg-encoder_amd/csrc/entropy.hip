@@ -82,6 +82,13 @@ __device__ __forceinline__ bool joined_tail(const Geom& g, int c) {
     return c == g.nch - 1 && g.more_after && g.restart_interval == 0;
 }
 
+// x mod d by a 16-bit reciprocal inv16 = ceil(2^16 / d): exact for x < 2^16 / d
+// (here x < 256 + 6, d = blocks per MCU <= 6) -- three full-rate instructions
+// instead of a division
+__device__ __forceinline__ int mod_small(int x, int d, uint32_t inv16) {
+    return x - d * (int)(__umul24((uint32_t)x, inv16) >> 16);
+}
+
 // One thread walks one block (64 zigzag coefficients held in 32 registers) in
 // stream order (encoder.rs:356-404; categorize.rs:132-169): DC code + extra bits,
 // then for each non-zero AC coefficient (run >> 4) ZRL codes and
@@ -347,6 +354,10 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     const int nb = span.nb;
     const long long e = (long long)frame * g.bpf + el0 + tid;
     const size_t cid = (size_t)frame * g.nch + chunk;
+    // the chunk's first block's place in its MCU (bpf < 2^31: 32-bit, once per
+    // wave) and a 16-bit reciprocal of the blocks per MCU for the per-lane mod
+    const int r0 = (int)((uint32_t)el0 % (uint32_t)g.bpm);
+    const uint32_t inv16 = (65536u + (uint32_t)g.bpm - 1u) / (uint32_t)g.bpm;
     // every global load of the prologue is issued before any is used (one latency,
     // not three): the code tables -- code_tab is [luma DC][luma AC][chroma DC]
     // [chroma AC] x 256; two AC words per thread, one DC word for threads below 32
@@ -406,7 +417,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             zigzag_in_registers(b);
             const int dp = dcdiff[ep];
             DMMT_TRACE(4);
-            const int kp = ((int)(el0 % g.bpm) + p) % g.bpm;
+            const int kp = mod_small(r0 + p, g.bpm, inv16);
             const bool lum = kp < g.n_luma;
             // the wave's walk stops after the last position any of its blocks uses
             const int kmax = __builtin_amdgcn_readfirstlane((int)sKey[min(64 * wave + 63, nb - 1)]);
@@ -421,7 +432,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     // a block too long for its slot sends the whole chunk down the re-walk path
     const bool over = __syncthreads_or(slot_over) != 0;
     const uint32_t bits = valid ? sBits[tid] : 0u;
-    const int k = valid ? ((int)(el0 % g.bpm) + tid) % g.bpm : 0;
+    const int k = valid ? mod_small(r0 + tid, g.bpm, inv16) : 0;
     const bool lum_t = k < g.n_luma;
     // offsets inside the chunk by a workgroup scan
     const uint32_t incl = wave_incl_scan_full_u32(bits);

@@ -38,8 +38,12 @@ constexpr int kPpmThreads = 256;
 constexpr int kPpmChunk = kPpmWin * kPpmThreads;  // bytes per workgroup
 constexpr int kPpmTail = 256;                  // bytes staged past the chunk for tokens running on
 constexpr int kPpmCarryThreads = 1024;
-constexpr int kFastWin = 64;                        // comment-free path: bytes per thread
-constexpr int kFastChunk = kFastWin * kPpmThreads;  // and per workgroup
+// comment-free path: a chunk is kFastPieces 16-byte pieces per thread (8 KB: the
+// parse kernel's LDS of 16.5 KB keeps 8 workgroups per CU); the count kernel
+// takes kCountChunks chunks per workgroup (4 pieces per thread)
+constexpr int kFastPieces = 2;
+constexpr int kFastChunk = 16 * kFastPieces * kPpmThreads;
+constexpr int kCountChunks = 2;
 
 // Transition maps: entry state s = (in comment) << 1 | (last kept byte a token
 // byte); entry s occupies bits [16s, 16s + 16): exit state << 14 | tokens started.
@@ -235,19 +239,21 @@ __device__ __forceinline__ uint32_t nondigit_bytes(uint32_t x) {
 // launcher guarantees t.len - t.safe >= 96); fix_pieces then rebuilds a piece that
 // crosses an end of the body byte by byte: bytes outside [lo, len) read as ' ' and
 // are never fetched.
-__device__ __forceinline__ void issue_pieces(const PpmText& t, long long c0, int tid, uint4 (&v)[4], bool (&full)[4]) {
+template <int P>
+__device__ __forceinline__ void issue_pieces(const PpmText& t, long long c0, int tid, uint4 (&v)[P], bool (&full)[P]) {
     const long long s16 = (t.safe + 15) & ~15ll;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < P; ++q) {
         const long long pos = c0 + 16 * (tid + kPpmThreads * q);
         full[q] = pos >= t.lo && pos + 16 <= t.len;
         v[q] = *reinterpret_cast<const uint4*>(t.text + (full[q] ? pos : s16));
     }
 }
-__device__ __forceinline__ void fix_pieces(const PpmText& t, long long c0, int tid, const uint4 (&v)[4],
-                                           const bool (&full)[4], uint32_t (&w)[4][4]) {
+template <int P>
+__device__ __forceinline__ void fix_pieces(const PpmText& t, long long c0, int tid, const uint4 (&v)[P],
+                                           const bool (&full)[P], uint32_t (&w)[P][4]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < P; ++q) {
         w[q][0] = v[q].x, w[q][1] = v[q].y, w[q][2] = v[q].z, w[q][3] = v[q].w;
         if (!full[q]) {
             const long long pos = c0 + 16 * (tid + kPpmThreads * q);
@@ -332,53 +338,67 @@ struct PpmReport {
     unsigned long long tokens;
 };
 
-__global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* __restrict__ counts) {
-    __shared__ uint32_t sRed[kPpmThreads / 64], sF[kPpmThreads / 64], sL[kPpmThreads / 64];
+__global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* __restrict__ counts,
+                                                           PpmReport* __restrict__ rep) {
+    constexpr int NW = kPpmThreads / 64, P = kFastPieces * kCountChunks;
+    __shared__ uint32_t sRed[NW][kCountChunks], sF[NW], sL[NW];
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const long long c0 = (long long)blockIdx.x * kFastChunk;
-    uint4 v[4];
-    bool full[4];
-    issue_pieces(t, c0, tid, v, full);
-    const uint32_t bb = load_byte_clamped(t, c0 - 1);  // the byte before the chunk
-    uint32_t w[4][4];
-    fix_pieces(t, c0, tid, v, full, w);
+    // chunks kCountChunks * bx + h, h = q / kFastPieces for piece q (the pieces of a
+    // chunk are consecutive in q, so piece q's predecessor is the same formula
+    // across the chunks of the workgroup)
+    const long long c0 = (long long)blockIdx.x * kCountChunks * kFastChunk;
+    uint4 v[P];
+    bool full[P];
+    issue_pieces<P>(t, c0, tid, v, full);
+    const uint32_t bb = load_byte_clamped(t, c0 - 1);  // the byte before the first chunk
+    uint32_t w[P][4];
+    fix_pieces<P>(t, c0, tid, v, full, w);
     const uint32_t before = body_sig(t, c0 - 1, bb);  // a token running in from the previous chunk
     // starts of each piece as if the byte before it were whitespace; fb / lb: whether
     // piece q's first / last byte is a token byte
-    uint32_t n = 0, fb = 0, lb = 0;
+    // bad: a token byte that is not a digit ('+', '#', anything else) -- the parse
+    // pass then hands the body to the general path (this memory-bound pass checks
+    // it for free)
+    uint32_t n[kCountChunks] = {}, fb = 0, lb = 0, bad = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < P; ++q) {
         uint32_t prev = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t s = sig_bytes(w[q][k]);
-            n += (uint32_t)__popc(starts_of(s, prev));
+            bad |= s & nondigit_bytes(w[q][k]);
+            n[q / kFastPieces] += (uint32_t)__popc(starts_of(s, prev));
             prev = s;
             if (k == 0) fb |= ((s >> 7) & 1u) << q;
             if (k == 3) lb |= (s >> 31) << q;
         }
     }
     // piece (q, lane) follows piece (q, lane - 1): a token across the seam counted twice
-    n -= (uint32_t)__popc(fb & lane_prev_u32(lb));  // (lane 0: 0)
-    n = wave_sum_full_u32(n);
-    if (lane == 0) {
-        sRed[wave] = n;
-        sF[wave] = fb;
+    const uint32_t seam = fb & lane_prev_u32(lb);  // (lane 0: 0)
+#pragma unroll
+    for (int h = 0; h < kCountChunks; ++h) {
+        const uint32_t m = ((1u << kFastPieces) - 1u) << (h * kFastPieces);
+        const uint32_t c = wave_sum_full_u32(n[h] - (uint32_t)__popc(seam & m));
+        if (lane == 0) sRed[wave][h] = c;
     }
+    if (lane == 0) sF[wave] = fb;
     if (lane == 63) sL[wave] = lb;
+    if (bad) reinterpret_cast<volatile uint32_t*>(&rep->bad)[0] = 1u;
     __syncthreads();
-    if (tid == 0) {  // the seams at each wave's lane 0: piece (q, 64 w - 1), or (q - 1, 255)
+    if (tid < kCountChunks) {  // the seams at each wave's lane 0: piece (q, 64 w - 1), or (q - 1, 255)
+        const int h = tid;
         uint32_t c = 0;
 #pragma unroll
-        for (int v = 0; v < kPpmThreads / 64; ++v) {
-            c += sRed[v];
+        for (int v = 0; v < NW; ++v) {
+            c += sRed[v][h];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t pb = v ? (sL[v - 1] >> q) & 1u : (q ? (sL[kPpmThreads / 64 - 1] >> (q - 1)) & 1u : before);
+            for (int q = h * kFastPieces; q < (h + 1) * kFastPieces; ++q) {
+                const uint32_t pb = v ? (sL[v - 1] >> q) & 1u : (q ? (sL[NW - 1] >> (q - 1)) & 1u : before);
                 c -= (sF[v] >> q) & pb & 1u;
             }
         }
-        counts[blockIdx.x] = c;
+        const long long k = (long long)blockIdx.x * kCountChunks + h;
+        if (k < t.nfast) counts[k] = c;
     }
 }
 
@@ -389,189 +409,204 @@ __device__ __forceinline__ uint32_t digits4(uint32_t d) {
     return __umul24(a, 10u) + (d >> 24);
 }
 
+// One chunk's global loads, issued together (see k_ppm_fast)
+struct FastLoads {
+    uint4 v[kFastPieces];
+    bool full[kFastPieces];
+    uint32_t tw;        // the next chunk's first 16 bytes: a word for each of threads 0-3
+    bool tfull;
+    uint32_t bb;        // the byte before the chunk
+    uint32_t cfirst;    // wave 0: a count of the chunk's row
+    unsigned long long rbase;
+};
+
 template <typename Out>
 __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* __restrict__ rep,
                                                           const uint32_t* __restrict__ counts,
                                                           const unsigned long long* __restrict__ row_base,
                                                           long long per, Out* __restrict__ out,
                                                           unsigned long long nsamples, uint32_t maxval) {
-    constexpr int NW = kPpmThreads / 64;
-    __shared__ uint32_t sText[kFastChunk / 4 + 4];  // the chunk (' ' outside the body) + the next 16 bytes
-    __shared__ uint16_t sIdx[kFastChunk / 2];      // token starts (chunk offsets) in text order
-    __shared__ uint32_t sScan[NW][2];
+    constexpr int NW = kPpmThreads / 64, P = kFastPieces;
+    // the chunk (' ' outside the body) + the next 16 bytes, staged for the
+    // neighbouring pieces' bytes; after the scan the same LDS holds the token
+    // entries in text order (at most one token per two bytes)
+    __shared__ uint32_t sLds[kFastChunk / 2];
+    uint32_t* const sText = sLds;
+    uint32_t* const sTok = sLds;
+    static_assert(kFastChunk / 4 + 4 <= kFastChunk / 2, "the staged text fits the entry array");
+    __shared__ uint32_t sScan[NW];
     __shared__ unsigned long long sBase;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-    const long long c0 = (long long)blockIdx.x * kFastChunk;
-    const long long row0 = (long long)(blockIdx.x / per) * per, bx = (long long)blockIdx.x;
-    // every load of the prologue is issued before any is used: the pieces, the next
-    // chunk's first 16 bytes (a word for each of threads 0-3), the byte before the
-    // chunk, and for the first token's index the row's base + the counts before this
-    // chunk in its row (wave 0)
-    uint4 v[4];
-    bool full[4];
-    issue_pieces(t, c0, tid, v, full);
-    const long long tp = c0 + kFastChunk + 4 * (tid & 3);
-    const bool tfull = tp >= t.lo && tp + 4 <= t.len;
-    uint32_t tw = *reinterpret_cast<const uint32_t*>(t.text + (tfull ? tp : (t.safe + 15) & ~15ll));
-    const uint32_t bb = load_byte_clamped(t, c0 - 1);
-    const uint32_t cfirst = counts[min(row0 + lane, bx)];
-    const unsigned long long rbase = row_base[blockIdx.x / per];
-    uint32_t cnt = row0 + lane < bx ? cfirst : 0u;
-    if (wave == 0) {
-        for (long long r0 = row0 + 64; r0 < bx; r0 += 64) {  // rows of more than 64 chunks (texts > 1 GB)
-            const uint32_t c = counts[min(r0 + lane, bx)];
-            cnt += r0 + lane < bx ? c : 0u;
+    // One workgroup per chunk (8 per CU).  Every global load is issued before any
+    // is used: the pieces, the next chunk's first 16 bytes, the byte before the
+    // chunk, and for its first token's index its row's base + the counts before it
+    // in its row.  (Resident workgroups looping over chunks with the next chunk's
+    // loads in flight measured slower: 6 per CU for the registers, 63 vs 49 us.)
+    auto issue = [&](long long c, FastLoads& f) {
+        const long long c0 = c * kFastChunk;
+        issue_pieces<P>(t, c0, tid, f.v, f.full);
+        const long long tp = c0 + kFastChunk + 4 * (tid & 3);
+        f.tfull = tp >= t.lo && tp + 4 <= t.len;
+        f.tw = *reinterpret_cast<const uint32_t*>(t.text + (f.tfull ? tp : (t.safe + 15) & ~15ll));
+        f.bb = load_byte_clamped(t, c0 - 1);
+        const long long row0 = (c / per) * per;
+        f.cfirst = counts[min(row0 + lane, c)];
+        f.rbase = row_base[c / per];
+    };
+    uint32_t bad = 0;  // a long token that does not parse (non-digit bytes: k_ppm_count)
+    uint32_t over = 0;
+    FastLoads cur;
+    const long long c = blockIdx.x;
+    issue(c, cur);
+    {
+        const long long c0 = c * kFastChunk;
+        const long long row0 = (c / per) * per;
+        uint32_t w[P][4];
+        fix_pieces<P>(t, c0, tid, cur.v, cur.full, w);
+        const uint32_t before = body_sig(t, c0 - 1, cur.bb);
+        uint32_t tw = cur.tw;
+        if (!cur.tfull) {
+            const long long tp = c0 + kFastChunk + 4 * (tid & 3);
+            tw = 0x20202020u;
+            for (int j = 0; j < 4; ++j)
+                if (tp + j >= t.lo && tp + j < t.len) tw = (tw & ~(0xFFu << (8 * j))) | ((uint32_t)t.text[tp + j] << (8 * j));
         }
-    }
-    uint32_t w[4][4];
-    fix_pieces(t, c0, tid, v, full, w);
-    const uint32_t before = body_sig(t, c0 - 1, bb);
-    if (!tfull) {
-        tw = 0x20202020u;
-        for (int j = 0; j < 4; ++j)
-            if (tp + j >= t.lo && tp + j < t.len) tw = (tw & ~(0xFFu << (8 * j))) | ((uint32_t)t.text[tp + j] << (8 * j));
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        reinterpret_cast<uint4*>(sText)[tid + kPpmThreads * q] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
-    if (tid < 4) sText[kFastChunk / 4 + tid] = tw;
-    __syncthreads();
-    // token starts per word; a piece's previous byte is the last of piece (q, t - 1):
-    // a lane shuffle, or for a wave's lane 0 the staged byte (the byte before the
-    // chunk for piece 0)
-    uint32_t st[4][4];
-    uint32_t n01 = 0, n23 = 0;  // starts per piece, two 16-bit fields each
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t s[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s[k] = sig_bytes(w[q][k]);
-        uint32_t prev = lane_prev_u32(s[3]);
-        if (lane == 0) {
-            const int p = tid + kPpmThreads * q;
-            const uint32_t pb = p ? (uint32_t)!ppm_ws((sText[(4 * p - 1)] >> 24)) : before;
-            prev = pb << 31;
-        }
-        uint32_t nq = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            st[q][k] = starts_of(s[k], prev);
-            prev = s[k];
-            nq += (uint32_t)__popc(st[q][k]);
-        }
-        if (q < 2)
-            n01 |= nq << (16 * q);
-        else
-            n23 |= nq << (16 * (q - 2));
-    }
-    const uint32_t i01 = wave_incl_scan_full_u32(n01), i23 = wave_incl_scan_full_u32(n23);
-    if (lane == 63) {
-        sScan[wave][0] = i01;
-        sScan[wave][1] = i23;
-    }
-    if (wave == 0) {
-        cnt = wave_sum_full_u32(cnt);
-        if (lane == 0) sBase = rbase + cnt;
-    }
-    __syncthreads();
-    uint32_t e01 = i01 - n01, e23 = i23 - n23, t01 = 0, t23 = 0;
-#pragma unroll
-    for (int v = 0; v < NW; ++v) {
-        e01 += v < wave ? sScan[v][0] : 0u;
-        e23 += v < wave ? sScan[v][1] : 0u;
-        t01 += sScan[v][0];
-        t23 += sScan[v][1];
-    }
-    const uint32_t T0 = t01 & 0xFFFFu, T1 = t01 >> 16, T2 = t23 & 0xFFFFu, T3 = t23 >> 16;
-    const uint32_t ntok = T0 + T1 + T2 + T3;
-    uint32_t rank[4] = {e01 & 0xFFFFu, T0 + (e01 >> 16), T0 + T1 + (e23 & 0xFFFFu), T0 + T1 + T2 + (e23 >> 16)};
-#if DMMT_PPM_ABL == 1  // study: the time up to the compaction
-    if (ntok == 12345678u) rep->bad = 1u;
-    return;
-#endif
-    // compaction: at most two starts per word (a start follows whitespace)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t off = 16u * (uint32_t)(tid + kPpmThreads * q);
-        uint32_t r = rank[q];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t m = st[q][k];
-            if (m) {
-                sIdx[r] = (uint16_t)(off + 4 * k + (__builtin_ctz(m) >> 3));
-                const uint32_t last = (uint32_t)(31 - __clz((int)m)) >> 3;
-                if (m & (m - 1u)) sIdx[r + 1] = (uint16_t)(off + 4 * k + last);
-                r += (uint32_t)__popc(m);
+        uint32_t cnt = row0 + lane < c ? cur.cfirst : 0u;
+        if (wave == 0) {
+            for (long long r0 = row0 + 64; r0 < c; r0 += 64) {  // rows of more than 64 chunks (texts > 512 MB)
+                const uint32_t x = counts[min(r0 + lane, c)];
+                cnt += r0 + lane < c ? x : 0u;
             }
         }
-    }
-    __syncthreads();
-#if DMMT_PPM_ABL == 2  // study: the time up to the token loop
-    if (sIdx[tid] == 12345u) rep->bad = 1u;
-    return;
-#endif
-    // one thread per token, two tokens (i, i + 256) per iteration so that their
-    // LDS reads overlap; the common case (at most 4 digits) is branch-free, and the
-    // loop makes no global loads (a token of 9 or more digits is only marked here
-    // and walked afterwards), so its stores are never waited for inside it
-    const unsigned long long base = sBase;
-    uint32_t bad = 0, over = 0, longm = 0;
-    // a token's value from the chunk words at its start: v, whether it parsed, or
-    // (long) 9+ digits to walk
-    auto token = [&](uint32_t s, uint32_t lo, uint32_t hi, uint32_t& v, bool& ok, bool& lng) {
-        const uint32_t j = s >> 2, r = s & 3u;
-        const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, r);  // token bytes 0-3
-        const uint32_t nd = nondigit_bytes(x);
-        const uint32_t L = nd ? (uint32_t)__builtin_ctz(nd) >> 3 : 4u;  // leading digits (of these 4)
-        const uint32_t b4 = __builtin_amdgcn_ubfe(hi, 8 * r, 8);       // token byte 4
-        uint32_t tb = L < 4 ? __builtin_amdgcn_ubfe(x, (8 * L) & 31, 8) : b4;  // the byte after the digits
-        v = digits4((x & 0x0F0F0F0Fu) << ((32 - 8 * L) & 31));
-        lng = false;
-        if (L == 4 && tb - 0x30u < 10u) {  // 5 or more digits: bytes 4-7 (u16 samples)
-            const uint32_t h2 = sText[j + 2];
-            const uint32_t y = __builtin_amdgcn_alignbyte(h2, hi, r);
-            const uint32_t nd2 = nondigit_bytes(y);
-            const uint32_t L2 = nd2 ? (uint32_t)__builtin_ctz(nd2) >> 3 : 4u;  // >= 1
-            tb = L2 < 4 ? __builtin_amdgcn_ubfe(y, (8 * L2) & 31, 8) : __builtin_amdgcn_ubfe(h2, 8 * r, 8);
-            const uint32_t p10 = L2 == 1 ? 10u : L2 == 2 ? 100u : L2 == 3 ? 1000u : 10000u;
-            v = v * p10 + digits4((y & 0x0F0F0F0Fu) << ((32 - 8 * L2) & 31));
-            lng = L2 == 4 && tb - 0x30u < 10u;  // 9 or more
+        const unsigned long long rbase = cur.rbase;
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+            reinterpret_cast<uint4*>(sText)[tid + kPpmThreads * q] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
+        if (tid < 4) sText[kFastChunk / 4 + tid] = tw;
+        __syncthreads();
+        // token starts per word; a piece's previous byte is the last of piece (q, t - 1):
+        // a lane shuffle, or for a wave's lane 0 the staged byte (the byte before the
+        // chunk for piece 0)
+        static_assert(P == 2, "the per-piece counts are scanned as two 16-bit fields");
+        uint32_t st[P][4], sg[P][4], wnext[P], snext[P];
+        uint32_t n01 = 0;  // starts per piece, two 16-bit fields
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sg[q][k] = sig_bytes(w[q][k]);  // (non-digit token bytes: k_ppm_count)
+            // the neighbouring pieces: the previous one's last byte (lane shuffle; a
+            // wave's lane 0 reads the staged byte, piece 0 the byte before the chunk)
+            // and the next one's first word (lane shuffle; lane 63 reads it staged:
+            // the next wave's lane 0 or, past the chunk, the next chunk's first bytes)
+            const int p = tid + kPpmThreads * q;
+            uint32_t prev = lane_prev_u32(sg[q][3]);
+            wnext[q] = lane_next_u32(w[q][0]);
+            if (lane == 0) {
+                const uint32_t pb = p ? (uint32_t)!ppm_ws((sText[(4 * p - 1)] >> 24)) : before;
+                prev = pb << 31;
+            }
+            if (lane == 63) wnext[q] = sText[4 * (p + 1)];
+            snext[q] = sig_bytes(wnext[q]);
+            uint32_t nq = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                st[q][k] = starts_of(sg[q][k], prev);
+                prev = sg[q][k];
+                nq += (uint32_t)__popc(st[q][k]);
+            }
+            n01 |= nq << (16 * q);
         }
-        // char::is_ascii_whitespace(tb): ' ', or one of \t \n \x0C \r (bits 9, 10, 12, 13)
-        const bool ws = tb == 0x20u || (tb < 14u && ((0x3600u >> tb) & 1u));
-        ok = L > 0 && ws && v <= 65535u;
-    };
-    uint32_t i = (uint32_t)tid;
-    for (int m = 0; i < ntok; i += 2 * kPpmThreads, m += 2) {
-        const uint32_t i1 = i + kPpmThreads;
-        const bool has1 = i1 < ntok;
-        const uint32_t s0 = sIdx[i], s1 = sIdx[has1 ? i1 : i];
-        const uint32_t lo0 = sText[s0 >> 2], hi0 = sText[(s0 >> 2) + 1];
-        const uint32_t lo1 = sText[s1 >> 2], hi1 = sText[(s1 >> 2) + 1];
-        uint32_t v0, v1;
-        bool ok0, ok1, lg0, lg1;
-        token(s0, lo0, hi0, v0, ok0, lg0);
-        token(s1, lo1, hi1, v1, ok1, lg1);
-        longm |= (lg0 ? 1u << m : 0u) | (has1 && lg1 ? 2u << m : 0u);
-        lg1 = lg1 || !has1;
-        bad |= (!ok0 && !lg0) || (!ok1 && !lg1);
-        over |= (ok0 && !lg0 && v0 > maxval) || (ok1 && !lg1 && v1 > maxval);
-#if DMMT_PPM_ABL == 3  // study: the token loop without its stores
-        if (v0 + v1 == 0x12345u) out[0] = 1;
-#else
-        if (!lg0 && base + i < nsamples) out[base + i] = (Out)(sizeof(Out) == 1 ? min(v0, 255u) : min(v0, 65535u));
-        if (!lg1 && base + i1 < nsamples) out[base + i1] = (Out)(sizeof(Out) == 1 ? min(v1, 255u) : min(v1, 65535u));
-#endif
-    }
-    while (longm) {  // (rare) tokens of 9 or more digits: leading zeros, or a parse error
-        const int m = __builtin_ctz(longm);
-        longm &= longm - 1u;
-        const uint32_t k = (uint32_t)tid + kPpmThreads * (uint32_t)m;
-        bool ok;
-        const uint32_t v = parse_token_walk(t, nullptr, 0, c0 + sIdx[k], ok);
-        bad |= !ok;
-        over |= ok && v > maxval;
-        if (base + k < nsamples) out[base + k] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+        const uint32_t i01 = wave_incl_scan_full_u32(n01);
+        if (lane == 63) sScan[wave] = i01;
+        if (wave == 0) {
+            cnt = wave_sum_full_u32(cnt);
+            if (lane == 0) sBase = rbase + cnt;
+        }
+        __syncthreads();  // (also: every neighbour read of the staged text is done)
+        uint32_t e01 = i01 - n01, t01 = 0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+            e01 += v < wave ? sScan[v] : 0u;
+            t01 += sScan[v];
+        }
+        const uint32_t T0 = t01 & 0xFFFFu, T1 = t01 >> 16;
+        const uint32_t ntok = T0 + T1;
+        const uint32_t rank[P] = {e01 & 0xFFFFu, T0 + (e01 >> 16)};
+        const unsigned long long base = sBase;
+        // compaction: at most two starts per word (a start follows whitespace).  A
+        // token's entry is its first four bytes with everything from its terminating
+        // whitespace on zeroed -- its digits, which the thread of the token combines --
+        // or, for a token of four or more bytes, 0x80000000 | its chunk offset (its
+        // text is read back from global memory)
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const uint32_t off = 16u * (uint32_t)(tid + kPpmThreads * q);
+            uint32_t r = rank[q];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t m = st[q][k];
+                if (m) {
+                    const uint32_t wn = k < 3 ? w[q][k + 1] : wnext[q];
+                    const uint32_t wsw = ~sg[q][k] & 0x80808080u, wsn = ~(k < 3 ? sg[q][k + 1] : snext[q]) & 0x80808080u;
+                    auto entry = [&](uint32_t a) {
+                        const uint32_t x = __builtin_amdgcn_alignbyte(wn, w[q][k], a);
+                        const uint32_t ws = __builtin_amdgcn_alignbyte(wsn, wsw, a);  // 0x80: whitespace byte
+                        const uint32_t keep = ((ws & (0u - ws)) >> 7) - 1u;           // the bytes before the first
+                        return ws ? x & keep : 0x80000000u | (off + 4 * k + a);
+                    };
+                    sTok[r] = entry((uint32_t)__builtin_ctz(m) >> 3);
+                    if (m & (m - 1u)) sTok[r + 1] = entry((uint32_t)(31 - __clz((int)m)) >> 3);
+                    r += (uint32_t)__popc(m);
+                }
+            }
+        }
+        __syncthreads();
+        // one thread per token: the entry's digits (the text of a token of four or
+        // more bytes is read back from global memory, its terminator checked there)
+        Out* const ob = out + base;
+        const uint32_t lim = base < nsamples ? (uint32_t)min((unsigned long long)ntok, nsamples - base) : 0u;
+        for (uint32_t i = (uint32_t)tid; i < ntok; i += kPpmThreads) {
+            const uint32_t e = sTok[i];
+            uint32_t v;
+            if (!(e & 0x80000000u)) {  // 1-3 digits: e's bytes past them are zero
+                const uint32_t L = (uint32_t)(32 - __clz((int)e) + 7) >> 3;
+                v = digits4((e & 0x0F0F0F0Fu) << (32 - 8 * L));
+            } else {  // four or more bytes (u16 samples, leading zeros)
+                const long long ps = c0 + (e & 0xFFFFu);
+                const long long pa = ps & ~3ll;
+                bool ok = true;
+                if (pa + 12 <= t.len) {
+                    uint32_t tw3[3];
+#pragma unroll
+                    for (int u = 0; u < 3; ++u) tw3[u] = *reinterpret_cast<const uint32_t*>(t.text + pa + 4 * u);
+                    const uint32_t r = (uint32_t)(ps & 3);
+                    const uint32_t x = __builtin_amdgcn_alignbyte(tw3[1], tw3[0], r);
+                    const uint32_t nd = nondigit_bytes(x);
+                    const uint32_t L = nd ? (uint32_t)__builtin_ctz(nd) >> 3 : 4u;
+                    uint32_t tb = L < 4 ? __builtin_amdgcn_ubfe(x, (8 * L) & 31, 8) : __builtin_amdgcn_ubfe(tw3[1], 8 * r, 8);
+                    v = digits4((x & 0x0F0F0F0Fu) << ((32 - 8 * L) & 31));
+                    ok = L > 0;
+                    if (L == 4 && tb - 0x30u < 10u) {  // 5 or more digits: bytes 4-7
+                        const uint32_t y = __builtin_amdgcn_alignbyte(tw3[2], tw3[1], r);
+                        const uint32_t nd2 = nondigit_bytes(y);
+                        const uint32_t L2 = nd2 ? (uint32_t)__builtin_ctz(nd2) >> 3 : 4u;  // >= 1
+                        tb = L2 < 4 ? __builtin_amdgcn_ubfe(y, (8 * L2) & 31, 8) : __builtin_amdgcn_ubfe(tw3[2], 8 * r, 8);
+                        const uint32_t p10 = L2 == 1 ? 10u : L2 == 2 ? 100u : L2 == 3 ? 1000u : 10000u;
+                        v = v * p10 + digits4((y & 0x0F0F0F0Fu) << ((32 - 8 * L2) & 31));
+                        if (L2 == 4 && tb - 0x30u < 10u) {  // 9 or more: walked
+                            v = parse_token_walk(t, nullptr, 0, ps, ok);
+                            tb = 0x20u;
+                        }
+                    }
+                    ok = ok && (tb == 0x20u || (tb < 14u && ((0x3600u >> tb) & 1u))) && v <= 65535u;
+                } else {  // the text's last bytes: walked
+                    v = parse_token_walk(t, nullptr, 0, ps, ok);
+                }
+                bad |= !ok;
+            }
+            over |= v > maxval;
+            if (i < lim) ob[i] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+        }
     }
     if (bad) reinterpret_cast<volatile uint32_t*>(&rep->bad)[0] = 1u;
     if (over) reinterpret_cast<volatile uint32_t*>(&rep->over)[0] = 1u;
@@ -787,14 +822,15 @@ hipError_t launch_ppm_p3_fast(const uint8_t* text, size_t body_offset, size_t le
     PpmReport* r = reinterpret_cast<PpmReport*>(report);
     const unsigned nfast = (unsigned)t.nfast;
     const long long rper = ppm_row_chunks(t.nfast);
-    hipLaunchKernelGGL(k_ppm_count, dim3(nfast), dim3(kPpmThreads), 0, st, t, counts);
+    hipLaunchKernelGGL(k_ppm_count, dim3((nfast + kCountChunks - 1) / kCountChunks), dim3(kPpmThreads), 0, st, t, counts, r);
     hipLaunchKernelGGL(k_ppm_rows, dim3(1), dim3(kPpmCarryThreads), 0, st, (const uint32_t*)counts, t.nfast, rper, r,
                        row_base);
+    const unsigned pgrid = nfast;
     if (sample_bytes == 1)
-        hipLaunchKernelGGL(k_ppm_fast<uint8_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, r, (const uint32_t*)counts,
+        hipLaunchKernelGGL(k_ppm_fast<uint8_t>, dim3(pgrid), dim3(kPpmThreads), 0, st, t, r, (const uint32_t*)counts,
                            (const unsigned long long*)row_base, rper, (uint8_t*)out, nsamples, maxval);
     else
-        hipLaunchKernelGGL(k_ppm_fast<uint16_t>, dim3(nfast), dim3(kPpmThreads), 0, st, t, r, (const uint32_t*)counts,
+        hipLaunchKernelGGL(k_ppm_fast<uint16_t>, dim3(pgrid), dim3(kPpmThreads), 0, st, t, r, (const uint32_t*)counts,
                            (const unsigned long long*)row_base, rper, (uint16_t*)out, nsamples, maxval);
     return hipGetLastError();
 }
