@@ -35,9 +35,12 @@ namespace dmmt {
         _dmmt_tr = _n;                                                    \
         _dmmt_tc = _c;                                                    \
     } while (0)
+#ifndef DMMT_TRACE_TID
+#define DMMT_TRACE_TID 0  // the thread whose marks are recorded (its wave's timeline)
+#endif
 #define DMMT_TRACE_FLUSH(base, span)                                      \
     do {                                                                  \
-        if (threadIdx.x == 0) {                                           \
+        if (threadIdx.x == DMMT_TRACE_TID) {                              \
             const unsigned long long _e = __builtin_amdgcn_s_memrealtime(); \
             atomicMax(&g_trace[48 + 4 * (span)], ~_dmmt_t0);              \
             atomicMax(&g_trace[49 + 4 * (span)], _e);                     \

@@ -86,7 +86,7 @@ __device__ __forceinline__ bool joined_tail(const Geom& g, int c) {
 // (here x < 256 + 6, d = blocks per MCU <= 6) -- three full-rate instructions
 // instead of a division
 __device__ __forceinline__ int mod_small(int x, int d, uint32_t inv16) {
-    return x - d * (int)(__umul24((uint32_t)x, inv16) >> 16);
+    return x - (int)__umul24((uint32_t)d, __umul24((uint32_t)x, inv16) >> 16);
 }
 
 // One thread walks one block (64 zigzag coefficients held in 32 registers) in
@@ -141,15 +141,17 @@ __device__ __forceinline__ void zigzag_in_registers(BlockCoef& b) {
     for (int j = 0; j < 32; ++j) b.w[j] = z[j];
 }
 
+// Code tables in LDS as (code, length) pairs: one ds_read_b64 per symbol gives
+// both halves with no masking or shifting.
 template <typename Sink>
-__device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const uint32_t* __restrict__ dctab,
-                                           const uint32_t* __restrict__ actab, Sink& sink, int kmax = 63) {
+__device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const uint2* __restrict__ dctab,
+                                           const uint2* __restrict__ actab, Sink& sink, int kmax = 63) {
     {
         const int cat = category_of(dcd);
-        const uint32_t e = dctab[cat];
-        sink(((e & 0xFFFFu) << cat) | extra_bits(dcd, cat), (int)(e >> 16) + cat);
+        const uint2 e = dctab[cat];
+        sink((e.x << cat) | extra_bits(dcd, cat), (int)e.y + cat);
     }
-    const uint32_t z = actab[0xF0];
+    const uint2 z = actab[0xF0];
     // l16 = 16 * (position of the last non-zero + 1): the zero run before position
     // k is r16 / 16 with r16 = 16 * k - l16, (run & 15) << 4 = r16 & 0xF0
     int l16 = 16;
@@ -163,16 +165,16 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
 #endif
         if (v != 0) {
             const int r16 = 16 * k - l16;
-            for (int r = r16 >> 8; r > 0; --r) sink(z & 0xFFFFu, (int)(z >> 16));
+            for (int r = r16 >> 8; r > 0; --r) sink(z.x, (int)z.y);
             const int cat = category_fast(v);
-            const uint32_t e = actab[(r16 & 0xF0) | cat];
-            sink(((e & 0xFFFFu) << cat) | extra_bits(v, cat), (int)(e >> 16) + cat);
+            const uint2 e = actab[(r16 & 0xF0) | cat];
+            sink((e.x << cat) | extra_bits(v, cat), (int)e.y + cat);
             l16 = 16 * k + 16;
         }
     }
     if (l16 < 16 * 64 || kmax < 63) {
-        const uint32_t e = actab[0];  // EOB
-        sink(e & 0xFFFFu, (int)(e >> 16));
+        const uint2 e = actab[0];  // EOB
+        sink(e.x, (int)e.y);
     }
 }
 
@@ -328,7 +330,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
                                               uint32_t* __restrict__ chunk_ff, uint32_t* __restrict__ chunk_edge,
                                               uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist) {
     // code tables: [luma AC 256][chroma AC 256][luma DC 16][chroma DC 16]
-    __shared__ uint32_t sTab[2 * 256 + 2 * 16];
+    __shared__ uint2 sTab[2 * 256 + 2 * 16];
     // the window image; during the sort and the walk its first words hold the
     // walk order, the keys and the blocks' bit counts (read before the window
     // loop, whose first clear follows two barriers)
@@ -369,10 +371,10 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     const uint32_t tdc = ct[((tt & 31) < 16 ? 0 : 512 - 16) + (tt & 31)];
     const uint32_t lz = lastnz[valid ? e : (long long)frame * g.bpf + el0];
     if (tid < 256) {
-        sTab[tid] = tac0;
-        sTab[256 + tid] = tac1;
+        sTab[tid] = make_uint2(tac0 & 0xFFFFu, tac0 >> 16);
+        sTab[256 + tid] = make_uint2(tac1 & 0xFFFFu, tac1 >> 16);
     }
-    if (tid < 32) sTab[512 + tid] = tdc;
+    if (tid < 32) sTab[512 + tid] = make_uint2(tdc & 0xFFFFu, tdc >> 16);
     if (chunk == 0) {  // the histogram replicas k_tables read: zero for the next launch
         for (int i = tid; i < kHistReps * 512; i += kEmitThreads) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
         for (int i = tid; i < kHistReps * 32; i += kEmitThreads) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
