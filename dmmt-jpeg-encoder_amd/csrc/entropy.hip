@@ -781,8 +781,30 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
     const int frame = blockIdx.y;
     const int c = blockIdx.x;
     const size_t cid = (size_t)frame * g.nch + c;
+    const bool last = c == g.nch - 1;
+    const size_t cidn = last ? cid : cid + 1;
+    // every global load of the prologue is issued before any is used: the frame's
+    // and the chunk's words, the next chunk's (its bits and edge for the shared last
+    // byte, its output offset for a closing RSTm), and this thread's slot words of
+    // the first pass -- word 4 tid on, whatever the chunk's first bit (which lies in
+    // the slot's first byte) -- so one latency, not four
     const uint32_t hdr = hdr_len[frame];
-    const unsigned long long end = (unsigned long long)hdr + total_out[frame];
+    const unsigned long long tot = total_out[frame];
+    const unsigned long long b0 = chunk_bit0[cid];
+    const uint32_t n = chunk_bits[cid], edge = chunk_edge[cid];
+    const uint32_t n_next = chunk_bits[cidn], edge_next = chunk_edge[cidn];
+    const unsigned long long cout = chunk_out[cid], cout_next = chunk_out[cidn];
+    const uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
+    uint32_t wv0[5];
+    {
+        const uint4 q = *reinterpret_cast<const uint4*>(slot + 4 * tid);
+        wv0[0] = q.x, wv0[1] = q.y, wv0[2] = q.z, wv0[3] = q.w;
+        wv0[4] = slot[4 * tid + 4];
+    }
+    // (the compiler would sink each load to its first use, past the branches below)
+    asm volatile("" ::"s"(hdr), "s"(tot), "s"(b0), "s"(n), "s"(edge), "s"(n_next), "s"(edge_next), "s"(cout),
+                 "s"(cout_next), "v"(wv0[0]), "v"(wv0[1]), "v"(wv0[2]), "v"(wv0[3]), "v"(wv0[4]));
+    const unsigned long long end = (unsigned long long)hdr + tot;
     if (end + 2 > out_stride) {  // uniform over the frame
         if (c == 0 && tid == 0) {
             out_len[frame] = 0;  // reported as DMMT_E_CAPACITY by the host
@@ -791,15 +813,14 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
         return;
     }
     const ChunkSpan sp = chunk_span(g, c);
-    const bool last = c == g.nch - 1;
     uint8_t* const base = out + (size_t)frame * out_stride + hdr;
     if (tid == 0) {
         if (last && !g.more_after) {  // EOI (encoder.rs:131) and the file size
-            base[total_out[frame]] = 0xFF;
-            base[total_out[frame] + 1] = 0xD9;
+            base[tot] = 0xFF;
+            base[tot + 1] = 0xD9;
             out_len[frame] = (uint32_t)(end + 2);
         } else if (sp.seg_last && g.restart_interval > 0) {  // RSTm closing restart segment m (extension; not stuffed)
-            const unsigned long long at = (last ? total_out[frame] : chunk_out[cid + 1]) - 2;
+            const unsigned long long at = (last ? tot : cout_next) - 2;
             base[at] = 0xFF;
             base[at + 1] = (uint8_t)(0xD0 + ((g.seg_base + sp.seg) & 7));
             if (last) out_len[frame] = (uint32_t)end;  // a stripe that more stripes follow
@@ -807,8 +828,6 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
             out_len[frame] = (uint32_t)end;  // a joined stripe that more stripes follow
         }
     }
-    const unsigned long long b0 = chunk_bit0[cid];
-    const uint32_t n = chunk_bits[cid];
     const unsigned long long e = b0 + n;
     const unsigned long long kbeg = (b0 + 7) >> 3, kend = (e + 7) >> 3;
     if (kend <= kbeg) return;  // a tail chunk inside the previous chunk's last byte
@@ -819,13 +838,12 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
     if (shared_tail) {
         const bool jt = joined_tail(g, c);
         const bool has_next = !sp.seg_last || jt;
-        tail = boundary_byte((int)(e & 7), chunk_edge[cid] & 0xFFFFu, has_next,
-                             jt ? (uint32_t)g.next_bits : (has_next ? chunk_bits[cid + 1] : 0u),
-                             jt ? g.next16 : (has_next ? chunk_edge[cid + 1] >> 16 : 0u));
+        tail = boundary_byte((int)(e & 7), edge & 0xFFFFu, has_next,
+                             jt ? (uint32_t)g.next_bits : (has_next ? n_next : 0u),
+                             jt ? g.next16 : (has_next ? edge_next >> 16 : 0u));
     }
-    const uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
     const unsigned off = (unsigned)(8 * kbeg - b0);  // the first owned byte starts this many bits into the chunk
-    uint8_t* o = base + chunk_out[cid];
+    uint8_t* o = base + cout;
     for (unsigned long long pos = 0; pos < nbytes; pos += kStuffPass) {  // uniform
         // the pass is staged at o's alignment (sOut[delta + i] = output byte i), so
         // it leaves LDS in aligned 16-byte stores
@@ -835,12 +853,12 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
         uint32_t x[4] = {0u, 0u, 0u, 0u};  // my 16 bytes, MSB first
         uint32_t cnt = 0;
         if (nvalid) {
-            const unsigned long long p = off + 8 * kb;  // bit position in the chunk stream
+            const unsigned long long p = off + 8 * kb;  // bit position in the chunk stream (off < 8)
             const size_t wi = (size_t)(p >> 5);
             const int sh = (int)(p & 31);
             uint32_t wv[5];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) wv[i] = slot[wi + i];
+            for (int i = 0; i < 5; ++i) wv[i] = pos ? slot[wi + i] : wv0[i];  // (pass 0: wi = 4 tid)
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = sh ? (wv[i] << sh) | (wv[i + 1] >> (32 - sh)) : wv[i];
             if (shared_tail && nbytes - 1 - kb < 16) {  // the shared / padded last byte

@@ -636,6 +636,9 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
         // kk is r16 / 16 with r16 = 16 * kk - l16, (run & 15) << 4 = r16 & 0xF0
         int l16 = 16;
         uint32_t zrl = 0;
+#ifdef DMMT_HIST_ABL
+        uint32_t abl = 0;
+#endif
 #pragma unroll
         for (int kk = 1; kk < 64; ++kk) {
             const int v = (kk & 1) ? ((int)b.w[kk >> 1] >> 16) : (int)(int16_t)(b.w[kk >> 1] & 0xFFFFu);
@@ -643,11 +646,18 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
                 if (CHECK && v == -32768) bad |= 4;
                 const int r16 = 16 * kk - l16;
                 zrl += (uint32_t)(r16 >> 8);
+#ifdef DMMT_HIST_ABL  // timing study: the walk's histogram atomics replaced by a register XOR
+                abl ^= (uint32_t)((r16 & 0xF0) | category_fast(v)) << (kk & 15);
+#else
                 atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
+#endif
                 l16 = 16 * kk + 16;
             }
         }
         if (zrl) atomicAdd(&h[0xF0], zrl);
+#ifdef DMMT_HIST_ABL
+        if (abl == 0x7FFFFFFFu) h[1] = abl;  // (keeps the XOR)
+#endif
         if (l16 < 16 * 64) atomicAdd(&h[0], 1u);  // EOB
         lastnz[e] = (uint8_t)((l16 >> 4) - 1);      // 0: no non-zero AC coefficient
         {
