@@ -335,6 +335,53 @@ def ppm_to_jpeg(enc, w, h, opts, opt_c, steps):
             "algorithmic_bytes": algo}
 
 
+def ppm_to_jpeg_stream(enc, w, h, opt_c, steps, lanes, distinct=3, per_call=12):
+    """The same path for a stream of files (dmmt_convert_ppm_device_batch, the
+    extension for serving): per call `per_call` files of w x h P3 text already in
+    HBM -> their JPEG files in HBM, decoded and encoded back to back over `lanes`
+    lanes with no synchronisation between files (the comment-free decode is checked
+    after the call).  The files rotate over `distinct` different frames' texts (3 x
+    90 MB at 4K: more than the 256 MB Infinity Cache).  Algorithmic bytes per file:
+    the text read once + the JPEG written once."""
+    texts = []
+    for k in range(distinct):
+        d_rgb = enc.malloc(w * h * 3)
+        enc.fill_synthetic(d_rgb, w, h, 1, first_frame=100 + k)
+        enc.synchronize()
+        rgb = np.frombuffer(enc.d2h(d_rgb, w * h * 3), np.uint8).reshape(h, w, 3)
+        enc.free(d_rgb)
+        text = p3_bytes(rgb)
+        d_text = enc.malloc(len(text))
+        enc.h2d(d_text, np.frombuffer(text, np.uint8))
+        texts.append((d_text, len(text), dmmt_jpeg.parse_ppm_header(text)))
+    cap = (dmmt_jpeg.max_jpeg_bytes(w, h, opt_c.subsampling) + 255) // 256 * 256
+    outs = [(enc.malloc(cap), enc.malloc(4)) for _ in range(per_call)]
+    files = [(texts[i % distinct][0], texts[i % distinct][1], texts[i % distinct][2], outs[i][0], cap, outs[i][1])
+             for i in range(per_call)]
+    enc.set_lanes(lanes)
+    try:
+        for _ in range(2):
+            enc.convert_ppm_device_batch(files, opt_c=opt_c)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            enc.convert_ppm_device_batch(files, opt_c=opt_c)
+        dt = (time.perf_counter() - t0) / (steps * per_call)
+        sizes = [int(np.frombuffer(enc.d2h(d_len, 4), np.uint32)[0]) for _, d_len in outs]
+    finally:
+        enc.set_lanes(1)
+        for d_out, d_len in outs:
+            enc.free(d_out)
+            enc.free(d_len)
+        for d_text, _, _ in texts:
+            enc.free(d_text)
+    algo = sum(t[1] for t in texts) / distinct + sum(sizes) / len(sizes)
+    return {"workload": f"{w}x{h} P3 texts ({distinct} distinct, {texts[0][1]} B) in HBM -> JPEG files in HBM, "
+                        f"{per_call} files per dmmt_convert_ppm_device_batch call over {lanes} lanes",
+            "ms_per_file": round(dt * 1e3, 4), "mpixel_per_s": round(w * h / dt / 1e6, 1),
+            "achieved_gbs": round(algo / dt / 1e9, 1), "frac": round(algo / dt / 1e9 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_file": round(algo)}
+
+
 def available_parallelism():
     """std::thread::available_parallelism() as the reference's CLI default uses it
     (cli.rs:104-109): the CPUs this process may run on, capped by a cgroup CPU
@@ -620,6 +667,8 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
         d = kern.get(dom, {})
         ingest = ppm_ingest(enc, w, h, args.ppm_steps) if args.ppm_steps > 0 else None
         ppm_jpeg = ppm_to_jpeg(enc, w, h, opts, opt_c, args.ppm_steps) if args.ppm_steps > 0 and fps == 1 else None
+        ppm_stream = (ppm_to_jpeg_stream(enc, w, h, opt_c, max(2, args.ppm_steps // 4), lanes)
+                      if args.ppm_steps > 0 and fps == 1 else None)
         cpu = None
         if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
             from oracle.synth import synthetic  # numpy twin of the device generator
@@ -675,6 +724,7 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
             "cpu_baseline": cpu,
             "ppm_ingest": ingest,
             "ppm_to_jpeg": ppm_jpeg,
+            "ppm_to_jpeg_stream": ppm_stream,
         }
         emit(json.dumps(line))
     for p in d_in + d_out + d_len:

@@ -68,6 +68,8 @@ struct Lane {
     int* dstatus = nullptr;  // its device address
     DevBuf coef, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
         chunk_edge, chunk_bit0, chunk_out;
+    // dmmt_convert_ppm_device_batch: a file's samples and its comment-free decode state
+    DevBuf ppm_rgb, ppm_counts, ppm_rowbase;
 };
 
 struct dmmt_ctx {
@@ -92,6 +94,8 @@ struct dmmt_ctx {
     // PPM ingest: file bytes, chunk maps / entry states, status + token count
     DevBuf ppm_text, ppm_maps, ppm_chunk_in, ppm_misc, ppm_counts;
     void* ppm_report = nullptr;  // host-mapped report of the comment-free P3 path (24 bytes)
+    void* ppm_batch_reports = nullptr;  // the same, one per file of dmmt_convert_ppm_device_batch
+    size_t ppm_batch_cap = 0;           // (files)
     // uploaded table state
     int lut_maxval = -1, lut_sb = -1;
     uint8_t q_cached[128];
@@ -476,7 +480,8 @@ void destroy_lane(Lane* L, bool own_stream) {
     if (L->status) (void)hipHostFree(L->status);
     DevBuf* bufs[] = {&L->coef,      &L->dcdiff,     &L->lastnz,     &L->ac_hist,
                       &L->dc_hist,  &L->code_tab,  &L->hdr_len,    &L->total_out,  &L->stage,
-                      &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out};
+                      &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out,
+                      &L->ppm_rgb,    &L->ppm_counts, &L->ppm_rowbase};
     for (DevBuf* b : bufs) release(*b);
     if (own_stream) (void)hipStreamDestroy(L->stream);
     delete L;
@@ -566,6 +571,7 @@ extern "C" void dmmt_ctx_destroy(dmmt_ctx* c) {
                       &c->ppm_counts};
     for (DevBuf* b : bufs) release(*b);
     if (c->ppm_report) (void)hipHostFree(c->ppm_report);
+    if (c->ppm_batch_reports) (void)hipHostFree(c->ppm_batch_reports);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -914,6 +920,128 @@ extern "C" int dmmt_decode_ppm_device(dmmt_ctx* c, const uint8_t* d_text, size_t
     int rc;
     if ((rc = set_device(c))) return rc;
     return decode_ppm(c, d_text, len, h, d_rgb, stream ? (hipStream_t)stream : c->stream);
+}
+
+// One file of dmmt_convert_ppm_device_batch on its own, on the context's stream, in
+// the reference's order: dmmt_decode_ppm_device's decode (its error precedence and
+// payload), then the image's checks and the encode, synchronised.  A file that
+// fails gets a zero size.
+static int convert_one_device(dmmt_ctx* c, const dmmt_ppm_file& f, const dmmt_options* opt) {
+    const dmmt_ppm_header& h = f.header;
+    const int sb = h.maxval > 255 ? 2 : 1;
+    const size_t frame = (size_t)h.width * h.height * 3 * (size_t)sb;
+    Lane* L = c->lanes[0];
+    int rc;
+    if ((rc = ensure(L->ppm_rgb, frame))) return rc;
+    rc = decode_ppm(c, f.d_text, f.len, &h, L->ppm_rgb.p, c->stream);
+    Geom g;
+    if (rc == DMMT_OK) rc = make_checked_geom(h.width, h.height, opt->subsampling, h.maxval, opt->restart_interval, &g);
+    if (rc == DMMT_OK && f.out_capacity < max_jpeg_bytes(g)) rc = DMMT_E_CAPACITY;
+    if (rc == DMMT_OK) {
+        if ((rc = enqueue_encode(c, L->ppm_rgb.p, frame, sb, 1, g, opt, f.d_out, f.out_capacity, f.d_out_len,
+                                 c->stream))) return rc;
+        rc = take_status(c, c->stream);
+    }
+    if (rc != DMMT_OK) {
+        HIP_TRY(hipMemsetAsync(f.d_out_len, 0, sizeof(uint32_t), c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return rc;
+}
+
+extern "C" int dmmt_convert_ppm_device_batch(dmmt_ctx* c, const dmmt_ppm_file* files, int n, const dmmt_options* opt,
+                                             int32_t* codes) {
+    c = primary(c);
+    dmmt::error_detail(DMMT_OK, 0);
+    if (!c || n < 0 || (n > 0 && (!files || !codes))) return DMMT_E_INVALID_ARGUMENT;
+    int rc;
+    if ((rc = validate(opt))) return rc;
+    if (n == 0) return DMMT_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = set_device(c))) return rc;
+    // earlier pipelined work's error bits are kept for dmmt_ctx_synchronize, so that
+    // the bits this batch raises are its own
+    for (Lane* L : c->lanes)
+        if ((rc = collect_async(c, L))) return rc;
+    if ((size_t)n > c->ppm_batch_cap) {
+        if (c->ppm_batch_reports) (void)hipHostFree(c->ppm_batch_reports);
+        c->ppm_batch_reports = nullptr;
+        c->ppm_batch_cap = 0;
+        HIP_TRY(hipHostMalloc(&c->ppm_batch_reports, (size_t)n * kPpmReportBytes,
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        c->ppm_batch_cap = (size_t)n;
+    }
+    uint8_t* const reps = (uint8_t*)c->ppm_batch_reports;
+    memset(reps, 0, (size_t)n * kPpmReportBytes);  // (no kernel is writing them: the lanes are idle)
+    uint8_t* dreps = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void**)&dreps, c->ppm_batch_reports, 0));
+    // state per file: 0 done (codes[i] final), 1 speculative fast-path P3 (report i), 2
+    // speculative P6, 3 redo on its own
+    std::vector<uint8_t> state((size_t)n, 0);
+    std::vector<int> lane_of((size_t)n, 0);
+    for (int i = 0; i < n; ++i) codes[i] = DMMT_OK;
+    for (int i = 0; i < n; ++i) {
+        const dmmt_ppm_file& f = files[i];
+        const dmmt_ppm_header& h = f.header;
+        if (!f.d_text || !f.d_out || !f.d_out_len || h.body_offset > f.len) {
+            codes[i] = DMMT_E_INVALID_ARGUMENT;
+            continue;
+        }
+        Geom g;
+        if (make_checked_geom(h.width, h.height, opt->subsampling, h.maxval, opt->restart_interval, &g) != DMMT_OK ||
+            f.out_capacity < max_jpeg_bytes(g)) {
+            state[i] = 3;  // the decode's error, if any, comes first: on its own
+            continue;
+        }
+        const unsigned long long ns = (unsigned long long)h.width * h.height * 3ull;
+        const int sb = h.maxval > 255 ? 2 : 1;
+        if (h.binary ? f.len - h.body_offset < ns * (unsigned long long)sb
+                     : !ppm_fast_path(f.d_text, h.body_offset, f.len)) {
+            state[i] = 3;  // a short P6 body's error, or a body too short for the fast path
+            continue;
+        }
+        const int lane = c->nlanes > 1 ? (int)(c->next_lane++ % (unsigned)c->nlanes) : 0;
+        Lane* L = c->lanes[lane];
+        hipStream_t st = L->stream;
+        lane_of[i] = lane;
+        if ((rc = ensure(L->ppm_rgb, ns * (size_t)sb))) return rc;
+        if (h.binary) {
+            HIP_TRY(launch_ppm_p6(f.d_text + h.body_offset, L->ppm_rgb.p, sb, ns, h.maxval, nullptr, st));
+            state[i] = 2;
+        } else {
+            const size_t nch = ppm_chunk_count(f.d_text, h.body_offset, f.len);
+            if ((rc = ensure(L->ppm_counts, ppm_counts_capacity((long long)nch) * 4))) return rc;
+            if ((rc = ensure(L->ppm_rowbase, std::max<size_t>(nch, 1024) * 8))) return rc;
+            HIP_TRY(launch_ppm_p3_fast(f.d_text, h.body_offset, f.len, (uint32_t*)L->ppm_counts.p,
+                                       (unsigned long long*)L->ppm_rowbase.p, dreps + (size_t)i * kPpmReportBytes,
+                                       L->ppm_rgb.p, sb, ns, h.maxval, st));
+            state[i] = 1;
+        }
+        // encoded at once, on the assumption that the decode succeeds (checked below)
+        if ((rc = enqueue_encode(c, L->ppm_rgb.p, ns * (size_t)sb, sb, 1, g, opt, f.d_out, f.out_capacity,
+                                 f.d_out_len, st, lane, true))) return rc;
+    }
+    std::vector<int> lane_bits(c->lanes.size(), 0);
+    for (size_t l = 0; l < c->lanes.size(); ++l)
+        if ((rc = read_status(c->lanes[l], kStatusAsync, c->lanes[l]->stream, &lane_bits[l]))) return rc;
+    for (int i = 0; i < n; ++i) {
+        if (state[i] == 0 || state[i] == 3) continue;
+        bool ok = lane_bits[lane_of[i]] == 0;  // an encode error on the lane: its files are redone
+        if (state[i] == 1) {
+            const volatile uint32_t* r = (const volatile uint32_t*)(reps + (size_t)i * kPpmReportBytes);
+            const unsigned long long tokens = (unsigned long long)r[4] | ((unsigned long long)r[5] << 32);
+            const unsigned long long ns = (unsigned long long)files[i].header.width * files[i].header.height * 3ull;
+            ok = ok && r[1] == 0u && r[2] == 0u && tokens == ns;  // else: the general path, or an error
+        }
+        state[i] = ok ? 0 : 3;
+    }
+    // the files the pipeline could not settle, one at a time with the exact error
+    int first = DMMT_OK;
+    for (int i = 0; i < n; ++i) {
+        if (state[i] == 3) codes[i] = convert_one_device(c, files[i], opt);
+        if (codes[i] != DMMT_OK && first == DMMT_OK) first = codes[i];
+    }
+    return first;
 }
 
 // convert_ppm_to_jpeg over several GPUs: the samples parsed on the host

@@ -52,6 +52,7 @@ hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t
 // 8 max(n, 1024) bytes each (n = ppm_chunk_count(...)).
 size_t ppm_chunk_count(const uint8_t* text, size_t body_offset, size_t len);
 size_t ppm_counts_capacity(long long nch);
+constexpr size_t kPpmReportBytes = 32;  // one comment-free report (24 bytes used)
 bool ppm_fast_path(const uint8_t* text, size_t body_offset, size_t len);
 hipError_t launch_ppm_p3_fast(const uint8_t* text, size_t body_offset, size_t len, uint32_t* counts,
                               unsigned long long* row_base, void* report, void* out, int sample_bytes,

@@ -100,6 +100,7 @@ def lib():
     L.dmmt_convert_ppm_to_jpeg.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, P(DmmtOptions)]
     L.dmmt_parse_ppm_header.argtypes = [vp, sz, P(DmmtPpmHeader)]
     L.dmmt_decode_ppm_device.argtypes = [vp, vp, sz, P(DmmtPpmHeader), vp, vp]
+    L.dmmt_convert_ppm_device_batch.argtypes = [vp, P(DmmtPpmFile), i32, P(DmmtOptions), P(i32)]
     L.dmmt_free.argtypes = [vp]
     L.dmmt_free.restype = None
     L.dmmt_strerror.argtypes = [ctypes.c_int]
@@ -174,6 +175,11 @@ class DmmtStripe(ctypes.Structure):
 class DmmtPpmHeader(ctypes.Structure):
     _fields_ = [("width", ctypes.c_uint16), ("height", ctypes.c_uint16), ("maxval", ctypes.c_uint16),
                 ("binary", ctypes.c_int32), ("body_offset", ctypes.c_uint64)]
+
+
+class DmmtPpmFile(ctypes.Structure):
+    _fields_ = [("d_text", ctypes.c_void_p), ("len", ctypes.c_size_t), ("header", DmmtPpmHeader),
+                ("d_out", ctypes.c_void_p), ("out_capacity", ctypes.c_size_t), ("d_out_len", ctypes.c_void_p)]
 
 
 STRIPE_HIST_WORDS = 2 * (16 + 256)
@@ -492,6 +498,24 @@ class Encoder:
         width*height*3 samples at d_rgb (uint8 if maxval <= 255 else uint16)"""
         _check(lib().dmmt_decode_ppm_device(self._ctx, d_text, length, ctypes.byref(header), d_rgb, stream),
                "decode_ppm_device")
+
+    def convert_ppm_device_batch(self, files, options: JpegTransformationOptions | None = None,
+                                 opt_c: DmmtOptions | None = None, check: bool = True):
+        """convert_ppm_to_jpeg (lib.rs:59-77) for files already in HBM, pipelined over
+        the lanes (dmmt_convert_ppm_device_batch).  files: (d_text, length, header,
+        d_out, out_capacity, d_out_len) tuples.  Returns the per-file codes; with
+        check, raises the first error."""
+        n = len(files)
+        arr = (DmmtPpmFile * max(n, 1))()
+        for i, (d_text, length, header, d_out, cap, d_len) in enumerate(files):
+            arr[i].d_text, arr[i].len, arr[i].header = d_text, length, header
+            arr[i].d_out, arr[i].out_capacity, arr[i].d_out_len = d_out, cap, d_len
+        codes = (ctypes.c_int32 * max(n, 1))()
+        opt = opt_c if opt_c is not None else options.to_c()
+        rc = lib().dmmt_convert_ppm_device_batch(self._ctx, arr, n, ctypes.byref(opt), codes)
+        if check:
+            _check(rc, "convert_ppm_device_batch")
+        return [codes[i] for i in range(n)]
 
     def read_ppm_device(self, data: bytes) -> Image:
         """PPMImageReader::read_image with the body decoded on the GPU: header on the

@@ -286,6 +286,28 @@ int dmmt_decode_ppm_device(dmmt_ctx* ctx, const uint8_t* d_text, size_t len, con
  * them on the GPU (dmmt_decode_ppm_device, then the encode path), write the file. */
 int dmmt_convert_ppm_to_jpeg(dmmt_ctx* ctx, const char* input_path, const char* output_path,
                              const dmmt_options* opt);
+/* Extension: convert_ppm_to_jpeg (lib.rs:59-77) for a stream of files already in device
+ * memory.  File i: its whole text (header included, parsed beforehand with
+ * dmmt_parse_ppm_header) -> its JPEG at d_out (out_capacity >= dmmt_max_jpeg_bytes(width,
+ * height, opt->subsampling)), the JPEG's size in *d_out_len (device memory).  The files are
+ * decoded and encoded back to back over the context's lanes (dmmt_ctx_set_lanes), with no
+ * synchronisation between files: a P3 body is decoded on the comment-free path on the
+ * assumption that it has no '#' and no error, and encoded at once; its report is checked
+ * after the batch, and a file whose body needs the general path (a comment, a '+' sign),
+ * or that fails, is redone on its own.  codes[i] receives file i's result: the code
+ * dmmt_decode_ppm_device and then the encode would return for it (a failed file's size is
+ * 0).  Returns the first non-zero code, DMMT_OK when every file succeeded; synchronised
+ * before returning.  dmmt_last_error_detail: the payload of the last file that failed. */
+typedef struct {
+    const uint8_t* d_text;   /* the whole file in device memory */
+    size_t len;
+    dmmt_ppm_header header;
+    uint8_t* d_out;
+    size_t out_capacity;
+    uint32_t* d_out_len;     /* device */
+} dmmt_ppm_file;
+int dmmt_convert_ppm_device_batch(dmmt_ctx* ctx, const dmmt_ppm_file* files, int32_t n, const dmmt_options* opt,
+                                  int32_t* codes);
 /* The payload the reference's Error variant carries (error.rs:3-22), for the last error a PPM
  * entry point (dmmt_parse_ppm, dmmt_read_ppm, dmmt_parse_ppm_header, dmmt_decode_ppm_device,
  * dmmt_convert_ppm_to_jpeg) returned on the calling thread: IncompletePixelParsed(n) -> n

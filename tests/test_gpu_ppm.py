@@ -222,3 +222,64 @@ def test_reference_ppm_unit_tests_on_gpu(encoder, name, text, err):
     assert e.value.code == err[0]
     if err[1] is not None:
         assert e.value.n == err[1]
+
+
+def test_convert_device_batch(encoder, spec_tables):
+    """dmmt_convert_ppm_device_batch: a stream of files in HBM decoded and encoded back
+    to back over three lanes, each file speculatively on the comment-free path; every
+    JPEG byte-identical to the oracle's and every code the one the file gets on its
+    own (host reader, then the encoder's range check): clean P3 files of several
+    sizes, comments (redone on the general path), 16-bit samples, P6, a token that
+    does not parse, an incomplete pixel, a body too short for the fast path, a sample
+    above maxval, a header too large for the output buffer."""
+    rng = np.random.default_rng(21)
+    cases = []  # (file bytes, samples or None, maxval)
+    for w, h in [(67, 45), (128, 96), (300, 211), (640, 360)]:
+        rgb = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        cases.append((p3_text(rgb, 255, rng), rgb, 255))
+    rgb = rng.integers(0, 256, (40, 52, 3), dtype=np.uint8)
+    cases.append((p3_text(rgb, 255, rng, comments=0.02, plus=0.02), rgb, 255))
+    rgb16 = rng.integers(0, 1001, (33, 41, 3), dtype=np.uint16)
+    cases.append((p3_text(rgb16, 1000, rng), rgb16, 1000))
+    rgb6 = rng.integers(0, 256, (7, 19, 3), dtype=np.uint8)
+    cases.append((b"P6 19 7 255\n" + rgb6.tobytes(), rgb6, 255))
+    cases.append((b"P3 2 2 255 " + b" ".join(b"%d" % v for v in range(11)) + b" x" + b" " * 100, None, 255))
+    cases.append((b"P3 2 4 255\n" + b"9 " * 23 + b" " * 100, None, 255))
+    small = np.array([[[1, 2, 3]]], np.uint8)
+    cases.append((b"P3 1 1 255 1 2 3", small, 255))
+    over = rng.integers(0, 201, (30, 40, 3), dtype=np.uint16)
+    over[5, 7, 1] = 250
+    cases.append((p3_text(over, 200, rng), over, 200))
+    cases = cases + cases[::-1]  # 22 files: every lane sees every kind
+    L = dmmt_jpeg.lib()
+    allocs, files, expect = [], [], []
+    try:
+        for k, (data, rgb, mx) in enumerate(cases):
+            hdr = dmmt_jpeg.parse_ppm_header(data)
+            cap = L.dmmt_max_jpeg_bytes(max(hdr.width, 1), max(hdr.height, 1), 2)
+            if k == 3:
+                cap -= 1  # too small: DMMT_E_CAPACITY after a successful decode
+            d_text, d_out, d_len = encoder.malloc(len(data)), encoder.malloc(cap), encoder.malloc(4)
+            allocs += [d_text, d_out, d_len]
+            encoder.h2d(d_text, np.frombuffer(data, np.uint8))
+            encoder.h2d(d_len, np.array([0xFFFFFFFF], np.uint32))
+            files.append((d_text, len(data), hdr, d_out, cap, d_len))
+            code = host_code(data)
+            if code == 0 and rgb is not None and int(rgb.max()) > mx:
+                code = -100  # DMMT_E_VALUE_EXCEEDS_MAX (color.rs:63-65)
+            if code == 0 and k == 3:
+                code = -203
+            expect.append((code, None if code else oracle.encode(rgb, mx, 2, *spec_tables)))
+        encoder.set_lanes(3)
+        codes = encoder.convert_ppm_device_batch(files, dmmt_jpeg.JpegTransformationOptions(), check=False)
+        assert codes == [e[0] for e in expect]
+        for (d_text, n, hdr, d_out, cap, d_len), (code, jpeg) in zip(files, expect):
+            size = int(np.frombuffer(encoder.d2h(d_len, 4), np.uint32)[0])
+            if code:
+                assert size == 0
+            else:
+                assert encoder.d2h(d_out, size) == jpeg
+    finally:
+        encoder.set_lanes(1)
+        for p in allocs:
+            encoder.free(p)
