@@ -930,9 +930,13 @@ static int convert_one_device(dmmt_ctx* c, const dmmt_ppm_file& f, const dmmt_op
     const dmmt_ppm_header& h = f.header;
     const int sb = h.maxval > 255 ? 2 : 1;
     const size_t frame = (size_t)h.width * h.height * 3 * (size_t)sb;
+    // no larger than what the text can fill (as dmmt_convert_ppm_to_jpeg): a
+    // successful decode needs the whole frame
+    const size_t body = f.len - (size_t)h.body_offset;
+    const size_t fit = (h.binary ? body / (size_t)sb : body / 2 + 1) * (size_t)sb;
     Lane* L = c->lanes[0];
     int rc;
-    if ((rc = ensure(L->ppm_rgb, frame))) return rc;
+    if ((rc = ensure(L->ppm_rgb, std::max<size_t>(std::min(frame, fit), 16)))) return rc;
     rc = decode_ppm(c, f.d_text, f.len, &h, L->ppm_rgb.p, c->stream);
     Geom g;
     if (rc == DMMT_OK) rc = make_checked_geom(h.width, h.height, opt->subsampling, h.maxval, opt->restart_interval, &g);
@@ -996,8 +1000,8 @@ extern "C" int dmmt_convert_ppm_device_batch(dmmt_ctx* c, const dmmt_ppm_file* f
         const unsigned long long ns = (unsigned long long)h.width * h.height * 3ull;
         const int sb = h.maxval > 255 ? 2 : 1;
         if (h.binary ? f.len - h.body_offset < ns * (unsigned long long)sb
-                     : !ppm_fast_path(f.d_text, h.body_offset, f.len)) {
-            state[i] = 3;  // a short P6 body's error, or a body too short for the fast path
+                     : !ppm_fast_path(f.d_text, h.body_offset, f.len) || ns > (f.len - h.body_offset) / 2 + 1) {
+            state[i] = 3;  // a body too short for its header (an error) or for the fast path
             continue;
         }
         const int lane = c->nlanes > 1 ? (int)(c->next_lane++ % (unsigned)c->nlanes) : 0;

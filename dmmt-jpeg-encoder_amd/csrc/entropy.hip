@@ -436,7 +436,18 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             // the wave's walk stops after the last position any of its blocks uses
             const int kmax = __builtin_amdgcn_readfirstlane((int)sKey[min(64 * wave + 63, nb - 1)]);
             SlotSink ss{sSlot + tid, 0ull, 0, 0};
+#ifdef DMMT_ABL_NOWALK  // timing bound: no symbol walk, ~5.5 bits per zigzag position up to lastnz
+            {
+                const int np = (int)sKey[tid] / 2 + 1;
+                uint32_t acc = b.w[0] ^ (uint32_t)dp;
+                for (int j = 0; j < np; ++j) acc ^= b.w[j & 31];
+                for (int j = 0; j < np; ++j) ss(acc & 0x7FFu, 11);
+                (void)kmax;
+                (void)lum;
+            }
+#else
             walk_block(b, dp, sTab + 512 + (lum ? 0 : 16), sTab + (lum ? 0 : 256), ss, kmax);
+#endif
             wbits = ss.finish();
             slot_over = wbits > (uint32_t)kSlotWords * 32u;
             sBits[p] = wbits;
@@ -670,6 +681,9 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
                                                   unsigned long long* __restrict__ total_out) {
     __shared__ unsigned long long sWave[16];
     __shared__ int sWaveF[16];
+#ifdef DMMT_PRIO_SMALL  // study: the one-workgroup kernels of a frame's chain ahead of other lanes' waves
+    __builtin_amdgcn_s_setprio(3);
+#endif
     const int tid = threadIdx.x;
     const int frame = blockIdx.x;
     const int nch = g.nch;

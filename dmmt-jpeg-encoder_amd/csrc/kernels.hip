@@ -639,6 +639,9 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
 #ifdef DMMT_HIST_ABL
         uint32_t abl = 0;
 #endif
+#ifdef DMMT_ABL_TOKW
+        uint32_t ntokw = 0;
+#endif
 #pragma unroll
         for (int kk = 1; kk < 64; ++kk) {
             const int v = (kk & 1) ? ((int)b.w[kk >> 1] >> 16) : (int)(int16_t)(b.w[kk >> 1] & 0xFFFFu);
@@ -646,6 +649,10 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
                 if (CHECK && v == -32768) bad |= 4;
                 const int r16 = 16 * kk - l16;
                 zrl += (uint32_t)(r16 >> 8);
+#ifdef DMMT_ABL_TOKW  // timing bound: a 32-bit symbol token stored per non-zero (over the block itself)
+                reinterpret_cast<uint32_t*>(const_cast<int16_t*>(coef))[e * 32 + 8 + (ntokw++ & 15)] =
+                    ((uint32_t)(r16 >> 8) << 24) | ((uint32_t)((r16 & 0xF0) | category_fast(v)) << 16) | ((uint32_t)v & 0xFFFFu);
+#endif
 #ifdef DMMT_HIST_ABL  // timing study: the walk's histogram atomics replaced by a register XOR
                 abl ^= (uint32_t)((r16 & 0xF0) | category_fast(v)) << (kk & 15);
 #else
@@ -780,6 +787,9 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
     __shared__ int sLeaf[PM_LEVELS];
     __shared__ uint32_t sWave[4];
     __shared__ int sBits[16];
+#ifdef DMMT_PRIO_SMALL  // study: the latency-bound tables ahead of other lanes' waves
+    __builtin_amdgcn_s_setprio(3);
+#endif
 
     DMMT_TRACE_START;
     const int tab = blockIdx.x, frame = blockIdx.y;

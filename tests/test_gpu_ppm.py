@@ -231,7 +231,8 @@ def test_convert_device_batch(encoder, spec_tables):
     own (host reader, then the encoder's range check): clean P3 files of several
     sizes, comments (redone on the general path), 16-bit samples, P6, a token that
     does not parse, an incomplete pixel, a body too short for the fast path, a sample
-    above maxval, a header too large for the output buffer."""
+    above maxval, a header too large for the output buffer, a short body whose
+    header claims 65535 x 65535 (no buffer is sized by the header)."""
     rng = np.random.default_rng(21)
     cases = []  # (file bytes, samples or None, maxval)
     for w, h in [(67, 45), (128, 96), (300, 211), (640, 360)]:
@@ -250,13 +251,16 @@ def test_convert_device_batch(encoder, spec_tables):
     over = rng.integers(0, 201, (30, 40, 3), dtype=np.uint16)
     over[5, 7, 1] = 250
     cases.append((p3_text(over, 200, rng), over, 200))
-    cases = cases + cases[::-1]  # 22 files: every lane sees every kind
+    cases.append((b"P3 65535 65535 255 " + b"7 " * 300, None, 255))  # a short body claiming a huge image
+    cases = cases + cases[::-1]  # 24 files: every lane sees every kind
     L = dmmt_jpeg.lib()
     allocs, files, expect = [], [], []
     try:
         for k, (data, rgb, mx) in enumerate(cases):
             hdr = dmmt_jpeg.parse_ppm_header(data)
             cap = L.dmmt_max_jpeg_bytes(max(hdr.width, 1), max(hdr.height, 1), 2)
+            if hdr.width * hdr.height > 1 << 24:
+                cap = 4096  # the huge header: its decode fails before the capacity check
             if k == 3:
                 cap -= 1  # too small: DMMT_E_CAPACITY after a successful decode
             d_text, d_out, d_len = encoder.malloc(len(data)), encoder.malloc(cap), encoder.malloc(4)
