@@ -217,3 +217,20 @@ def test_multi_gpu_c_driver():
         assert r.returncode == 0, r.stderr
         line = json.loads(r.stdout.strip().splitlines()[-1])
         assert line["match"] and line["members"] == int(args[4]) and line["batch"]["mismatched"] == 0
+
+
+def test_bench_inproc_leg_on_the_gpu():
+    """bench.py --inproc through the real C-ABI group (two members on GPU 0): the
+    contract's one JSON line, every member's pixels counted, JPEGs of the
+    workload's size (the stand-in group of tests/test_bench_dist.py checks the
+    arithmetic; this runs the real dmmt_encode_device_multi pipeline)"""
+    import bench
+    lines = []
+    bench.main(["--inproc", "--devices", "0,0", "--steps", "4", "--warmup", "1", "--cpu-seconds", "0",
+                "--ppm-steps", "0"], emit=lines.append)
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["metric"] == "Mpixel/s encoded (4K PPM, q=90)" and d["n_gpus"] == 1 and d["steps"] == 4
+    assert d["config"]["members"] == 2 and d["config"]["device_ids"] == [0, 0]
+    assert d["value"] > 0 and d["scaling"] == "weak"
+    assert 4e6 < d["config"]["mean_jpeg_bytes"] < 7e6  # a 4K q90 synthetic frame: ~5.3 MB
