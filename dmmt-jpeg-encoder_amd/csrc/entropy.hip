@@ -408,7 +408,9 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     }
     __syncthreads();
     DMMT_TRACE(0);
+#ifdef DMMT_EMIT_COPY_LOOP
     int pw = 0;          // the block this thread walks
+#endif
     uint32_t wbits = 0;  // and its bits
     bool slot_over = false;
     {
@@ -424,7 +426,9 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         // one walk: the block's bits into this thread's private slot, and its bit count
         if (valid) {
             const int p = sOrder[tid];
+#ifdef DMMT_EMIT_COPY_LOOP
             pw = p;
+#endif
             const long long ep = (long long)frame * g.bpf + el0 + p;
             BlockCoef b;
             load_block(coef + ep * 64, b);
