@@ -685,9 +685,6 @@ __global__ __launch_bounds__(1024) void k_offsets(const uint32_t* __restrict__ c
                                                   unsigned long long* __restrict__ total_out) {
     __shared__ unsigned long long sWave[16];
     __shared__ int sWaveF[16];
-#ifdef DMMT_PRIO_SMALL  // study: the one-workgroup kernels of a frame's chain ahead of other lanes' waves
-    __builtin_amdgcn_s_setprio(3);
-#endif
     const int tid = threadIdx.x;
     const int frame = blockIdx.x;
     const int nch = g.nch;

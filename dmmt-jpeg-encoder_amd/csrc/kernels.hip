@@ -787,9 +787,6 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
     __shared__ int sLeaf[PM_LEVELS];
     __shared__ uint32_t sWave[4];
     __shared__ int sBits[16];
-#ifdef DMMT_PRIO_SMALL  // study: the latency-bound tables ahead of other lanes' waves
-    __builtin_amdgcn_s_setprio(3);
-#endif
 
     DMMT_TRACE_START;
     const int tab = blockIdx.x, frame = blockIdx.y;
