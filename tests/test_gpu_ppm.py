@@ -287,3 +287,61 @@ def test_convert_device_batch(encoder, spec_tables):
         encoder.set_lanes(1)
         for p in allocs:
             encoder.free(p)
+
+
+def _random_file(rng):
+    """a random small PPM file: P3 (separators, sometimes comments, signs, leading
+    zeros, a broken token, a missing or extra sample, a sample above maxval) or P6"""
+    w, h = int(rng.integers(1, 90)), int(rng.integers(1, 70))
+    mx = int(rng.choice([255, 255, 255, 100, 1000, 65535]))
+    rgb = rng.integers(0, mx + 1, (h, w, 3)).astype(np.uint16)
+    if mx < 65535 and rng.random() < 0.1:
+        rgb.reshape(-1)[int(rng.integers(0, rgb.size))] = mx + 1 + int(rng.integers(0, 5))
+    if rng.random() < 0.15 and mx == 255 and int(rgb.max()) <= 255:
+        return b"P6 %d %d 255\n" % (w, h) + rgb.astype(np.uint8).tobytes(), rgb, mx
+    r = rng.random()
+    data = p3_text(rgb, mx, rng, ws_max=int(rng.integers(1, 4)),
+                   comments=0.02 if r < 0.15 else 0.0, plus=0.02 if r < 0.25 else 0.0,
+                   zeros=0.03 if r < 0.35 else 0.0)
+    k = rng.random()
+    if k < 0.06:  # a token that does not parse
+        data = data[:-3] + b" 1x "
+    elif k < 0.12:  # one sample missing
+        data = data.rstrip()
+        data = data[:data.rfind(b" ") if b" " in data[-8:] else len(data)]
+    elif k < 0.16:  # one sample too many
+        data += b" 7 "
+    return data, rgb, mx
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_convert_device_batch_fuzz(encoder, spec_tables, seed):
+    """dmmt_convert_ppm_device_batch on 40 random files per seed, 1-4 lanes: every
+    code the host reader's (then the encoder's range check), every JPEG the
+    oracle's"""
+    rng = np.random.default_rng(100 + seed)
+    cases = [_random_file(rng) for _ in range(40)]
+    L = dmmt_jpeg.lib()
+    allocs, files, expect = [], [], []
+    try:
+        for data, rgb, mx in cases:
+            hdr = dmmt_jpeg.parse_ppm_header(data)
+            cap = L.dmmt_max_jpeg_bytes(max(hdr.width, 1), max(hdr.height, 1), 2)
+            d_text, d_out, d_len = encoder.malloc(len(data)), encoder.malloc(cap), encoder.malloc(4)
+            allocs += [d_text, d_out, d_len]
+            encoder.h2d(d_text, np.frombuffer(data, np.uint8))
+            files.append((d_text, len(data), hdr, d_out, cap, d_len))
+            code = host_code(data)
+            if code == 0 and int(rgb.max()) > mx:
+                code = -100
+            expect.append((code, None if code else oracle.encode(rgb, mx, 2, *spec_tables)))
+        encoder.set_lanes(int(rng.integers(1, 5)))
+        codes = encoder.convert_ppm_device_batch(files, dmmt_jpeg.JpegTransformationOptions(), check=False)
+        assert codes == [e[0] for e in expect]
+        for (d_text, n, hdr, d_out, cap, d_len), (code, jpeg) in zip(files, expect):
+            size = int(np.frombuffer(encoder.d2h(d_len, 4), np.uint32)[0])
+            assert size == 0 if code else encoder.d2h(d_out, size) == jpeg
+    finally:
+        encoder.set_lanes(1)
+        for p in allocs:
+            encoder.free(p)
