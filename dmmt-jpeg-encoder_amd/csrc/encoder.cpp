@@ -67,7 +67,7 @@ struct Lane {
     int* status = nullptr;   // [2][kStatusWords], host-mapped
     int* dstatus = nullptr;  // its device address
     DevBuf coef, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
-        chunk_edge, chunk_bit0, chunk_out;
+        chunk_edge, chunk_bit0, chunk_out, arrive;
     // dmmt_convert_ppm_device_batch: a file's samples and its comment-free decode state
     DevBuf ppm_rgb, ppm_counts, ppm_rowbase;
 };
@@ -241,6 +241,8 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     if ((rc = ensure(L->ac_hist, (size_t)nf * kHistReps * 512 * 4, true))) return rc;
     if ((rc = ensure(L->dc_hist, (size_t)nf * kHistReps * 32 * 4, true))) return rc;
     if ((rc = ensure(L->code_tab, (size_t)nf * 1024 * 4))) return rc;
+    // k_emit's arrival counters: zero from the allocation, reset by each frame's last workgroup
+    if ((rc = ensure(L->arrive, (size_t)nf * kArriveFrameWords * 4, true))) return rc;
     if ((rc = ensure(L->hdr_len, (size_t)nf * 4))) return rc;
     if ((rc = ensure(L->total_out, (size_t)nf * 8))) return rc;
     if (!L->status) {
@@ -268,6 +270,7 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     w->chunk_bit0 = (unsigned long long*)L->chunk_bit0.p;
     w->chunk_out = (unsigned long long*)L->chunk_out.p;
     w->total_out = (unsigned long long*)L->total_out.p;
+    w->arrive = (uint32_t*)L->arrive.p;
     w->status = L->dstatus + (async ? kStatusAsync : kStatusSync) * kStatusWords;
     w->norm_lut = nullptr;  // bound by prepare() after upload_tables
     w->qtab = nullptr;
@@ -350,9 +353,9 @@ int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bit
     }
     {
         StageTimer t(c, ST_EMIT, st);
-        HIP_TRY(launch_emit(nf, g, w, st));
+        HIP_TRY(launch_emit(nf, g, w, true, st));
     }
-    {
+    if (!offsets_fusable(g)) {  // (else k_emit's last workgroup computed them)
         StageTimer t(c, ST_OFFSETS, st);
         HIP_TRY(launch_offsets(nf, g, w, st));
     }
@@ -480,7 +483,7 @@ void destroy_lane(Lane* L, bool own_stream) {
     if (L->status) (void)hipHostFree(L->status);
     DevBuf* bufs[] = {&L->coef,      &L->dcdiff,     &L->lastnz,     &L->ac_hist,
                       &L->dc_hist,  &L->code_tab,  &L->hdr_len,    &L->total_out,  &L->stage,
-                      &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out,
+                      &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out, &L->arrive,
                       &L->ppm_rgb,    &L->ppm_counts, &L->ppm_rowbase};
     for (DevBuf* b : bufs) release(*b);
     if (own_stream) (void)hipStreamDestroy(L->stream);
@@ -1474,7 +1477,7 @@ extern "C" int dmmt_stripe_measure(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STR
     }
     {
         StageTimer t(c, ST_EMIT, s);
-        HIP_TRY(launch_emit(1, g, w, s));
+        HIP_TRY(launch_emit(1, g, w, false, s));  // (the joined stripe's offsets wait for its seam: dmmt_stripe_write)
     }
     std::vector<uint32_t> nb((size_t)g.nch), edge((size_t)g.nch);
     HIP_TRY(hipMemcpyAsync(nb.data(), w.chunk_bits, nb.size() * 4, hipMemcpyDeviceToHost, s));

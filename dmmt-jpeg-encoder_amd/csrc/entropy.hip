@@ -325,13 +325,28 @@ __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
     return (uint32_t)(x >> (48 - (p & 31))) & 0xFFFFu;
 }
 
+__device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ cff,
+                              const uint32_t* __restrict__ cedge, const Geom& g, unsigned long long* __restrict__ bit0,
+                              unsigned long long* __restrict__ outo, unsigned long long* __restrict__ total,
+                              unsigned long long* sWaveV, int* sWaveF);
+constexpr int kArriveGroups = 64, kArriveStride = 32;                 // counters 128 bytes apart
+constexpr int kArriveWords = (kArriveGroups + 1) * kArriveStride;  // per frame (kernels.hpp: kArriveFrameWords)
+static_assert(kArriveWords == kArriveFrameWords, "the host sizes the counters");
+
 // ---------------------------------------------------------------------- k_emit
+// fuse: the frame's last workgroup to finish also computes every chunk's offsets
+// (fused_offsets; `arrive` counts the finished workgroups per frame and is zero
+// between launches), so no k_offsets launch follows
 __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* coef, const int16_t* __restrict__ dcdiff,
                                               const uint8_t* __restrict__ lastnz,
                                               const uint32_t* __restrict__ code_tab, Geom g,
                                               uint32_t* __restrict__ stage, uint32_t* __restrict__ chunk_bits,
                                               uint32_t* __restrict__ chunk_ff, uint32_t* __restrict__ chunk_edge,
-                                              uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist) {
+                                              uint32_t* __restrict__ ac_hist, uint32_t* __restrict__ dc_hist,
+                                              int fuse, uint32_t* __restrict__ arrive,
+                                              unsigned long long* __restrict__ chunk_bit0,
+                                              unsigned long long* __restrict__ chunk_out,
+                                              unsigned long long* __restrict__ total_out) {
     // code tables: [luma AC 256][chroma AC 256][luma DC 16][chroma DC 16]
     __shared__ uint2 sTab[2 * 256 + 2 * 16];
     // the window image; during the sort and the walk its first words hold the
@@ -343,6 +358,9 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     __shared__ uint32_t sBin[65];  // walk order: blocks counted, then started, by last non-zero position
+    __shared__ unsigned long long sOffV[kEmitWaves];  // fused offsets: the scans' wave totals
+    __shared__ int sOffF[kEmitWaves];
+    __shared__ uint32_t sLast;
 #ifdef DMMT_EMIT_COPY_LOOP
     __shared__ uint32_t sStart[kEmitThreads];  // bit offset of block t in the chunk
 #endif
@@ -557,16 +575,47 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         }
     }
     __syncthreads();
-    if (tid < 8) chunk_ff[cid * 8 + tid] = sFF[tid];
+    // the chunk's summary, stored write-through (agent scope): the frame's last
+    // workgroup reads it when the offsets are fused
+    if (tid < 8) __hip_atomic_store(chunk_ff + cid * 8 + tid, sFF[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) {
-        chunk_bits[cid] = total;
+        __hip_atomic_store(chunk_bits + cid, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t first16 = sEdge[0] >> 16;
         uint32_t last16;
         if (total >= 16)
             last16 = bits16_at(sEdge[1], sEdge[2], (int)(total - 16));
         else
             last16 = total ? sEdge[0] >> (32 - total) : 0u;
-        chunk_edge[cid] = (first16 << 16) | last16;
+        __hip_atomic_store(chunk_edge + cid, (first16 << 16) | last16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (fuse) {  // (uniform) count this workgroup in once its summary has reached memory
+        // Two levels of counters, each on its own 128-byte line: chunk c counts into
+        // group c mod kArriveGroups, the last of a group into the frame's top
+        // counter (atomics on one address serialise: 1519 on a single counter cost
+        // ~18 us); every counter is reset by its last arriver
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t* const fa = arrive + (size_t)frame * kArriveWords;
+            const int grp = (int)(chunk % kArriveGroups);
+            const int ngrp = min(g.nch, kArriveGroups);
+            const uint32_t in_grp = (uint32_t)((g.nch - grp + kArriveGroups - 1) / kArriveGroups);
+            bool last = false;
+            if (__hip_atomic_fetch_add(fa + grp * kArriveStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                in_grp - 1u) {
+                __hip_atomic_store(fa + grp * kArriveStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint32_t* const top = fa + kArriveGroups * kArriveStride;
+                last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)ngrp - 1u;
+                if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            sLast = last;
+        }
+        __syncthreads();
+        if (sLast) {  // every other chunk of the frame is done: its offsets
+            const size_t fb = (size_t)frame * g.nch;
+            fused_offsets(chunk_bits + fb, chunk_ff + fb * 8, chunk_edge + fb, g, chunk_bit0 + fb, chunk_out + fb,
+                          total_out + frame, sOffV, sOffF);
+        }
     }
     DMMT_TRACE(3);
     DMMT_TRACE_FLUSH(0, 0);
@@ -613,15 +662,16 @@ __device__ __forceinline__ unsigned long long chunk_out_bytes(const uint32_t* __
     return out;
 }
 
-// workgroup (1024 threads) exclusive scan; *tot receives the total
-__device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long v, unsigned long long* sWave,
-                                                              unsigned long long* tot) {
+// workgroup (NW waves) exclusive scan; *tot receives the total
+template <int NW>
+__device__ __forceinline__ unsigned long long block_scan_nw(unsigned long long v, unsigned long long* sWave,
+                                                            unsigned long long* tot) {
     const int lane = lane_id(), wave = threadIdx.x >> 6;
-    const unsigned long long incl = wave_incl_scan_full_u64(v);  // (all 1024 threads take part)
+    const unsigned long long incl = wave_incl_scan_full_u64(v);  // (every thread takes part)
     if (lane == 63) sWave[wave] = incl;
     __syncthreads();
     unsigned long long pre = incl - v, all = 0;
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < NW; ++q) {
         if (q < wave) pre += sWave[q];
         all += sWave[q];
     }
@@ -637,9 +687,10 @@ __device__ __forceinline__ void seg_combine(bool& f, unsigned long long& v, bool
     f = f || f2;
 }
 
-// workgroup (1024 threads) exclusive segmented scan of (flag, value)
-__device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigned long long v,
-                                                                 unsigned long long* sWaveV, int* sWaveF) {
+// workgroup (NW waves) exclusive segmented scan of (flag, value)
+template <int NW>
+__device__ __forceinline__ unsigned long long block_segscan_nw(bool f, unsigned long long v,
+                                                               unsigned long long* sWaveV, int* sWaveF) {
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     bool fi = f;
     unsigned long long vi = v;
@@ -674,6 +725,116 @@ __device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigne
     seg_combine(rf, rv, fe != 0, ve);
     __syncthreads();
     return rv;
+}
+
+__device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long v, unsigned long long* sWave,
+                                                              unsigned long long* tot) {
+    return block_scan_nw<16>(v, sWave, tot);
+}
+__device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigned long long v,
+                                                                 unsigned long long* sWaveV, int* sWaveF) {
+    return block_segscan_nw<16>(f, v, sWaveV, sWaveF);
+}
+
+// The chunk offsets of one frame computed by k_emit's last workgroup to finish
+// (frames of at most kFusedOffsetsMaxChunks chunks; k_offsets otherwise): what
+// k_offsets computes, with 256 threads and up to 6 chunks each in registers (8
+// spill at k_emit's 72 VGPRs).  The
+// other workgroups' summaries (bits, 0xFF counts, edges) were stored write-through
+// (agent scope) before they counted themselves in, so they are read with
+// agent-scope loads; the bit scan comes first, then only the 0xFF count at each
+// chunk's own alignment residue is loaded.
+static_assert(kFusedOffsetsMaxChunks % kEmitThreads == 0, "whole chunks per thread of the fused offsets");
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ cff,
+                              const uint32_t* __restrict__ cedge, const Geom& g, unsigned long long* __restrict__ bit0,
+                              unsigned long long* __restrict__ outo, unsigned long long* __restrict__ total,
+                              unsigned long long* sWaveV, int* sWaveF) {
+    // (a fused frame has at most 2048 chunks of at most 256 * 1984 bits: its bit and
+    // byte offsets fit 32 bits, which keeps the eight chunks' state in few registers)
+    constexpr int KP = kFusedOffsetsMaxChunks / kEmitThreads, NT = kEmitThreads;
+    const int tid = threadIdx.x;
+    const int nch = g.nch;
+    const int per = (nch + NT - 1) / NT;  // <= KP (the launcher's condition)
+    const int c0 = min(tid * per, nch), c1 = min(c0 + per, nch);
+    uint32_t nbits[KP], edge[KP];
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {  // every load issued before any is used (clamped indices)
+        const int c = min(c0 + i, nch - 1);
+        nbits[i] = ld_agent(cbits + c);
+        edge[i] = ld_agent(cedge + c);
+    }
+    const int cl = min(c1, nch - 1);  // the chunk after this thread's last
+    const uint32_t nlast = ld_agent(cbits + cl), elast = ld_agent(cedge + cl);
+    uint32_t firstm = 0, seglm = 0;  // per chunk i: bit i
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+        const int c = c0 + i;
+        if (c < c1) {
+            const ChunkSpan sp = chunk_span(g, c);
+            firstm |= (uint32_t)sp.seg_first << i;
+            seglm |= (uint32_t)sp.seg_last << i;
+        } else {
+            nbits[i] = 0u;
+        }
+    }
+    bool f = false;
+    unsigned long long v = 0;
+#pragma unroll
+    for (int i = 0; i < KP; ++i)
+        if (c0 + i < c1) seg_combine(f, v, (firstm >> i) & 1u, nbits[i] + (c0 + i == 0 ? (uint32_t)g.bit_phase : 0u));
+    uint32_t run = (uint32_t)block_segscan_nw<kEmitWaves>(f, v, sWaveV, sWaveF);
+    uint32_t b0[KP];
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+        b0[i] = 0;
+        if (c0 + i < c1) {
+            if ((firstm >> i) & 1u) run = c0 + i == 0 ? (uint32_t)g.bit_phase : 0u;
+            b0[i] = run;
+            run += nbits[i];
+        }
+    }
+    uint32_t ob[KP];
+#pragma unroll
+    for (int i = 0; i < KP; ++i)  // the 0xFF bytes inside the chunk at its actual alignment
+        ob[i] = ld_agent(cff + (size_t)min(c0 + i, nch - 1) * 8 + ((8 - (b0[i] & 7)) & 7));
+    uint32_t mine = 0;
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+        const int c = c0 + i;
+        if (c >= c1) {
+            ob[i] = 0;
+            continue;
+        }
+        const uint32_t e = b0[i] + nbits[i];
+        uint32_t o = ((e + 7) >> 3) - ((b0[i] + 7) >> 3) + ob[i];
+        if ((e & 7) && (e & ~7u) >= b0[i]) {
+            // the byte shared with the next chunk of the segment (or the padding)
+            const bool segl = (seglm >> i) & 1u;
+            const bool jt = segl && joined_tail(g, c);
+            const bool hasn = !segl || jt;
+            const uint32_t nn = jt ? (uint32_t)g.next_bits : i + 1 < KP && c + 1 < c1 ? nbits[min(i + 1, KP - 1)] : nlast;
+            const uint32_t en = jt ? g.next16 << 16 : i + 1 < KP && c + 1 < c1 ? edge[min(i + 1, KP - 1)] : elast;
+            const uint32_t byte = boundary_byte((int)(e & 7), edge[i] & 0xFFFFu, hasn, nn, en >> 16);
+            o += byte == 0xFFu ? 1u : 0u;
+        }
+        if (((seglm >> i) & 1u) && (c != nch - 1 || (g.more_after && g.restart_interval > 0))) o += 2;  // RSTm
+        ob[i] = o;
+        mine += o;
+    }
+    unsigned long long tot = 0;
+    uint32_t orun = (uint32_t)block_scan_nw<kEmitWaves>(mine, sWaveV, &tot);
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+        const int c = c0 + i;
+        if (c >= c1) continue;
+        bit0[c] = b0[i];
+        outo[c] = orun;
+        orun += ob[i];
+    }
+    if (tid == 0) *total = tot;
 }
 
 // -------------------------------------------------------------------- k_offsets
@@ -941,10 +1102,13 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
 }
 
 // --------------------------------------------------------------------- launchers
-hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t st) {
+bool offsets_fusable(const Geom& g) { return g.nch <= kFusedOffsetsMaxChunks; }
+
+hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_offsets, hipStream_t st) {
+    const int fuse = fuse_offsets && offsets_fusable(g) ? 1 : 0;
     hipLaunchKernelGGL(k_emit, dim3(g.nch, n_frames), dim3(kEmitThreads), 0, st, (const int16_t*)w.coef,
                        (const int16_t*)w.dcdiff, (const uint8_t*)w.lastnz, (const uint32_t*)w.code_tab, g, w.stage, w.chunk_bits, w.chunk_ff,
-                       w.chunk_edge, w.ac_hist, w.dc_hist);
+                       w.chunk_edge, w.ac_hist, w.dc_hist, fuse, w.arrive, w.chunk_bit0, w.chunk_out, w.total_out);
     return hipGetLastError();
 }
 

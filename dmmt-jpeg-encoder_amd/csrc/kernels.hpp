@@ -23,6 +23,7 @@ struct Work {
     unsigned long long* chunk_bit0; // [frames][nch] bit offset of the chunk in its restart segment
     unsigned long long* chunk_out;  // [frames][nch] offset of the chunk's output bytes after the header
     unsigned long long* total_out;  // [frames] stuffed scan bytes incl. RST markers
+    uint32_t* arrive;               // [frames][kArriveFrameWords] k_emit's finished workgroups (fused offsets), zero between launches
     int* status;                    // error words (raise_status): bit k of the error kinds -> word k; 1 value>max, 2 table, 4 category range, 16 output capacity
     const float* norm_lut;          // maxval-normalisation table
     const float* qtab;              // [2][64] f32
@@ -38,7 +39,13 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st);
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st);
-hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, hipStream_t st);
+// fuse_offsets: when offsets_fusable(g), k_emit's last workgroup per frame also
+// computes the chunk offsets (chunk_bit0, chunk_out, total_out), and no
+// launch_offsets is needed; otherwise launch_offsets follows as before
+constexpr int kFusedOffsetsMaxChunks = 1536;  // (4K 4:4:4: 1519)
+constexpr int kArriveFrameWords = 65 * 32;  // k_emit's arrival counters per frame (Work::arrive)
+bool offsets_fusable(const Geom& g);
+hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_offsets, hipStream_t st);
 hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_t st);
 hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
                              uint32_t* out_len, hipStream_t st);
