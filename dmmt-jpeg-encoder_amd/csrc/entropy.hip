@@ -358,7 +358,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
     __shared__ uint32_t sBin[65];  // walk order: blocks counted, then started, by last non-zero position
-    __shared__ unsigned long long sOffV[kEmitWaves];  // fused offsets: the scans' wave totals
+    __shared__ unsigned long long sOffV[kEmitWaves + 1];  // fused offsets: the scans' wave totals, the carry
     __shared__ int sOffF[kEmitWaves];
     __shared__ uint32_t sLast;
 #ifdef DMMT_EMIT_COPY_LOOP
@@ -690,7 +690,8 @@ __device__ __forceinline__ void seg_combine(bool& f, unsigned long long& v, bool
 // workgroup (NW waves) exclusive segmented scan of (flag, value)
 template <int NW>
 __device__ __forceinline__ unsigned long long block_segscan_nw(bool f, unsigned long long v,
-                                                               unsigned long long* sWaveV, int* sWaveF) {
+                                                               unsigned long long* sWaveV, int* sWaveF,
+                                                               bool* flag_out = nullptr) {
     const int lane = lane_id(), wave = threadIdx.x >> 6;
     bool fi = f;
     unsigned long long vi = v;
@@ -724,6 +725,7 @@ __device__ __forceinline__ unsigned long long block_segscan_nw(bool f, unsigned 
     unsigned long long rv = cv;
     seg_combine(rf, rv, fe != 0, ve);
     __syncthreads();
+    if (flag_out) *flag_out = rf;
     return rv;
 }
 
@@ -738,13 +740,16 @@ __device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigne
 
 // The chunk offsets of one frame computed by k_emit's last workgroup to finish
 // (frames of at most kFusedOffsetsMaxChunks chunks; k_offsets otherwise): what
-// k_offsets computes, with 256 threads and up to 6 chunks each in registers (8
-// spill at k_emit's 72 VGPRs).  The
-// other workgroups' summaries (bits, 0xFF counts, edges) were stored write-through
-// (agent scope) before they counted themselves in, so they are read with
-// agent-scope loads; the bit scan comes first, then only the 0xFF count at each
-// chunk's own alignment residue is loaded.
-static_assert(kFusedOffsetsMaxChunks % kEmitThreads == 0, "whole chunks per thread of the fused offsets");
+// k_offsets computes, with 256 threads, in rounds of kFusedRoundChunks chunks (6
+// per thread in registers; 8 spill at k_emit's 72 VGPRs), each round carrying the
+// bit position and the byte count of the ones before it.  The other workgroups'
+// summaries (bits, 0xFF counts, edges) were stored write-through (agent scope)
+// before they counted themselves in, so they are read with agent-scope loads; the
+// bit scan comes first, then only the 0xFF count at each chunk's own alignment
+// residue is loaded.  sWaveV holds kEmitWaves + 1 words (the last: the carry).
+static_assert(kFusedRoundChunks % kEmitThreads == 0, "whole chunks per thread of the fused offsets");
+static_assert((unsigned long long)kFusedOffsetsMaxChunks * kChunkBlocks * kMaxBlockBits < (1ull << 32),
+              "a fused frame's bit offsets fit 32 bits");
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -752,89 +757,98 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
                               const uint32_t* __restrict__ cedge, const Geom& g, unsigned long long* __restrict__ bit0,
                               unsigned long long* __restrict__ outo, unsigned long long* __restrict__ total,
                               unsigned long long* sWaveV, int* sWaveF) {
-    // (a fused frame has at most 2048 chunks of at most 256 * 1984 bits: its bit and
-    // byte offsets fit 32 bits, which keeps the eight chunks' state in few registers)
-    constexpr int KP = kFusedOffsetsMaxChunks / kEmitThreads, NT = kEmitThreads;
+    // (32-bit offsets: the static_assert above; they keep the chunks' state in few registers)
+    constexpr int KP = kFusedRoundChunks / kEmitThreads, NT = kEmitThreads;
     const int tid = threadIdx.x;
     const int nch = g.nch;
-    const int per = (nch + NT - 1) / NT;  // <= KP (the launcher's condition)
-    const int c0 = min(tid * per, nch), c1 = min(c0 + per, nch);
-    uint32_t nbits[KP], edge[KP];
+    uint32_t carry_run = 0, carry_out = 0;  // the bit position after, and the bytes of, the rounds before
+    for (int r0 = 0; r0 < nch; r0 += kFusedRoundChunks) {  // uniform
+        const int rn = min(kFusedRoundChunks, nch - r0);
+        const int per = (rn + NT - 1) / NT;  // <= KP
+        const int c0 = r0 + min(tid * per, rn), c1 = r0 + min(tid * per + per, rn);
+        uint32_t nbits[KP], edge[KP];
 #pragma unroll
-    for (int i = 0; i < KP; ++i) {  // every load issued before any is used (clamped indices)
-        const int c = min(c0 + i, nch - 1);
-        nbits[i] = ld_agent(cbits + c);
-        edge[i] = ld_agent(cedge + c);
-    }
-    const int cl = min(c1, nch - 1);  // the chunk after this thread's last
-    const uint32_t nlast = ld_agent(cbits + cl), elast = ld_agent(cedge + cl);
-    uint32_t firstm = 0, seglm = 0;  // per chunk i: bit i
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-        const int c = c0 + i;
-        if (c < c1) {
-            const ChunkSpan sp = chunk_span(g, c);
-            firstm |= (uint32_t)sp.seg_first << i;
-            seglm |= (uint32_t)sp.seg_last << i;
-        } else {
-            nbits[i] = 0u;
+        for (int i = 0; i < KP; ++i) {  // every load issued before any is used (clamped indices)
+            const int c = min(c0 + i, nch - 1);
+            nbits[i] = ld_agent(cbits + c);
+            edge[i] = ld_agent(cedge + c);
         }
-    }
-    bool f = false;
-    unsigned long long v = 0;
+        const int cl = min(c1, nch - 1);  // the chunk after this thread's last
+        const uint32_t nlast = ld_agent(cbits + cl), elast = ld_agent(cedge + cl);
+        uint32_t firstm = 0, seglm = 0;  // per chunk i: bit i
 #pragma unroll
-    for (int i = 0; i < KP; ++i)
-        if (c0 + i < c1) seg_combine(f, v, (firstm >> i) & 1u, nbits[i] + (c0 + i == 0 ? (uint32_t)g.bit_phase : 0u));
-    uint32_t run = (uint32_t)block_segscan_nw<kEmitWaves>(f, v, sWaveV, sWaveF);
-    uint32_t b0[KP];
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-        b0[i] = 0;
-        if (c0 + i < c1) {
-            if ((firstm >> i) & 1u) run = c0 + i == 0 ? (uint32_t)g.bit_phase : 0u;
-            b0[i] = run;
-            run += nbits[i];
+        for (int i = 0; i < KP; ++i) {
+            const int c = c0 + i;
+            if (c < c1) {
+                const ChunkSpan sp = chunk_span(g, c);
+                firstm |= (uint32_t)sp.seg_first << i;
+                seglm |= (uint32_t)sp.seg_last << i;
+            } else {
+                nbits[i] = 0u;
+            }
         }
-    }
-    uint32_t ob[KP];
+        bool f = false;
+        unsigned long long v = 0;
 #pragma unroll
-    for (int i = 0; i < KP; ++i)  // the 0xFF bytes inside the chunk at its actual alignment
-        ob[i] = ld_agent(cff + (size_t)min(c0 + i, nch - 1) * 8 + ((8 - (b0[i] & 7)) & 7));
-    uint32_t mine = 0;
+        for (int i = 0; i < KP; ++i)
+            if (c0 + i < c1) seg_combine(f, v, (firstm >> i) & 1u, nbits[i] + (c0 + i == 0 ? (uint32_t)g.bit_phase : 0u));
+        bool fx;
+        const uint32_t ex = (uint32_t)block_segscan_nw<kEmitWaves>(f, v, sWaveV, sWaveF, &fx);
+        uint32_t run = fx ? ex : carry_run + ex;  // (a segment start before it in this round resets the carry)
+        uint32_t b0[KP];
 #pragma unroll
-    for (int i = 0; i < KP; ++i) {
-        const int c = c0 + i;
-        if (c >= c1) {
-            ob[i] = 0;
-            continue;
+        for (int i = 0; i < KP; ++i) {
+            b0[i] = 0;
+            if (c0 + i < c1) {
+                if ((firstm >> i) & 1u) run = c0 + i == 0 ? (uint32_t)g.bit_phase : 0u;
+                b0[i] = run;
+                run += nbits[i];
+            }
         }
-        const uint32_t e = b0[i] + nbits[i];
-        uint32_t o = ((e + 7) >> 3) - ((b0[i] + 7) >> 3) + ob[i];
-        if ((e & 7) && (e & ~7u) >= b0[i]) {
-            // the byte shared with the next chunk of the segment (or the padding)
-            const bool segl = (seglm >> i) & 1u;
-            const bool jt = segl && joined_tail(g, c);
-            const bool hasn = !segl || jt;
-            const uint32_t nn = jt ? (uint32_t)g.next_bits : i + 1 < KP && c + 1 < c1 ? nbits[min(i + 1, KP - 1)] : nlast;
-            const uint32_t en = jt ? g.next16 << 16 : i + 1 < KP && c + 1 < c1 ? edge[min(i + 1, KP - 1)] : elast;
-            const uint32_t byte = boundary_byte((int)(e & 7), edge[i] & 0xFFFFu, hasn, nn, en >> 16);
-            o += byte == 0xFFu ? 1u : 0u;
-        }
-        if (((seglm >> i) & 1u) && (c != nch - 1 || (g.more_after && g.restart_interval > 0))) o += 2;  // RSTm
-        ob[i] = o;
-        mine += o;
-    }
-    unsigned long long tot = 0;
-    uint32_t orun = (uint32_t)block_scan_nw<kEmitWaves>(mine, sWaveV, &tot);
+        if (c0 < c1 && c1 == r0 + rn) sWaveV[kEmitWaves] = run;  // the round's last chunk: the next carry
+        uint32_t ob[KP];
 #pragma unroll
-    for (int i = 0; i < KP; ++i) {
-        const int c = c0 + i;
-        if (c >= c1) continue;
-        bit0[c] = b0[i];
-        outo[c] = orun;
-        orun += ob[i];
+        for (int i = 0; i < KP; ++i)  // the 0xFF bytes inside the chunk at its actual alignment
+            ob[i] = ld_agent(cff + (size_t)min(c0 + i, nch - 1) * 8 + ((8 - (b0[i] & 7)) & 7));
+        uint32_t mine = 0;
+#pragma unroll
+        for (int i = 0; i < KP; ++i) {
+            const int c = c0 + i;
+            if (c >= c1) {
+                ob[i] = 0;
+                continue;
+            }
+            const uint32_t e = b0[i] + nbits[i];
+            uint32_t o = ((e + 7) >> 3) - ((b0[i] + 7) >> 3) + ob[i];
+            if ((e & 7) && (e & ~7u) >= b0[i]) {
+                // the byte shared with the next chunk of the segment (or the padding)
+                const bool segl = (seglm >> i) & 1u;
+                const bool jt = segl && joined_tail(g, c);
+                const bool hasn = !segl || jt;
+                const uint32_t nn = jt ? (uint32_t)g.next_bits : i + 1 < KP && c + 1 < c1 ? nbits[min(i + 1, KP - 1)] : nlast;
+                const uint32_t en = jt ? g.next16 << 16 : i + 1 < KP && c + 1 < c1 ? edge[min(i + 1, KP - 1)] : elast;
+                const uint32_t byte = boundary_byte((int)(e & 7), edge[i] & 0xFFFFu, hasn, nn, en >> 16);
+                o += byte == 0xFFu ? 1u : 0u;
+            }
+            if (((seglm >> i) & 1u) && (c != nch - 1 || (g.more_after && g.restart_interval > 0))) o += 2;  // RSTm
+            ob[i] = o;
+            mine += o;
+        }
+        unsigned long long tot = 0;
+        uint32_t orun = carry_out + (uint32_t)block_scan_nw<kEmitWaves>(mine, sWaveV, &tot);  // (its barriers publish the carry)
+#pragma unroll
+        for (int i = 0; i < KP; ++i) {
+            const int c = c0 + i;
+            if (c >= c1) continue;
+            bit0[c] = b0[i];
+            outo[c] = orun;
+            orun += ob[i];
+        }
+        carry_out += (uint32_t)tot;
+        carry_run = (uint32_t)sWaveV[kEmitWaves];
+        __syncthreads();  // (the carry word is rewritten by the next round)
     }
-    if (tid == 0) *total = tot;
+    if (tid == 0) *total = carry_out;
 }
 
 // -------------------------------------------------------------------- k_offsets

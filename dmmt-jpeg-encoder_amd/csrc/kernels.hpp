@@ -42,7 +42,8 @@ hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_pe
 // fuse_offsets: when offsets_fusable(g), k_emit's last workgroup per frame also
 // computes the chunk offsets (chunk_bit0, chunk_out, total_out), and no
 // launch_offsets is needed; otherwise launch_offsets follows as before
-constexpr int kFusedOffsetsMaxChunks = 1536;  // (4K 4:4:4: 1519)
+constexpr int kFusedRoundChunks = 1536;       // per round of the fused scan (4K 4:4:4: 1519 chunks, one round)
+constexpr int kFusedOffsetsMaxChunks = 4 * kFusedRoundChunks;  // (8K 4:2:0: 3038 chunks, two rounds)
 constexpr int kArriveFrameWords = 65 * 32;  // k_emit's arrival counters per frame (Work::arrive)
 bool offsets_fusable(const Geom& g);
 hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_offsets, hipStream_t st);
