@@ -663,6 +663,8 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
             except ValueError:
                 pmc = None
         kern = kernel_roofline(prof, algo_bytes, fps, pmc)
+        if "k_emit" in kern and "k_offsets" not in kern:  # frames of <= 6144 chunks
+            kern["k_emit"]["includes"] = "the frame's chunk-offset scans (k_offsets fused into its last workgroup)"
         dom = max(kern, key=lambda k: kern[k]["avg_launch_us"]) if kern else None
         d = kern.get(dom, {})
         ingest = ppm_ingest(enc, w, h, args.ppm_steps) if args.ppm_steps > 0 else None
