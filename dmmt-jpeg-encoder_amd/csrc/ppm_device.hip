@@ -409,6 +409,52 @@ __device__ __forceinline__ uint32_t digits4(uint32_t d) {
     return __umul24(a, 10u) + (d >> 24);
 }
 
+// A short token's entry (its 1-3 ASCII digits in bytes 0-2, the bytes past them
+// zero) -> its value.  The digits' weights are 100/10/1 shifted down by the bytes
+// the token lacks: an ASCII digit's top byte has two leading zeros, so the entry's
+// leading-zero count is 10, 18 or 26 for 3, 2 or 1 digits, and (clz + 22) mod 32 is
+// the shift 0, 8 or 16.
+__device__ __forceinline__ uint32_t short_token(uint32_t e) {
+    const uint32_t sh = ((uint32_t)__builtin_clz(e) + 22u) & 31u;  // (no entry is zero)
+    return __builtin_amdgcn_udot4(e & 0x0F0F0F0Fu, 0x00010A64u >> sh, 0u, false);
+}
+
+// A token of four or more bytes at text position ps (read back from global memory,
+// its digits and terminator checked there), as str::parse::<u16>
+__device__ __forceinline__ uint32_t long_token(const PpmText& t, long long ps, bool& ok) {
+    const long long pa = ps & ~3ll;
+    uint32_t v;
+    ok = true;
+    if (pa + 12 <= t.len) {
+        uint32_t tw3[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) tw3[u] = *reinterpret_cast<const uint32_t*>(t.text + pa + 4 * u);
+        const uint32_t r = (uint32_t)(ps & 3);
+        const uint32_t x = __builtin_amdgcn_alignbyte(tw3[1], tw3[0], r);
+        const uint32_t nd = nondigit_bytes(x);
+        const uint32_t L = nd ? (uint32_t)__builtin_ctz(nd) >> 3 : 4u;
+        uint32_t tb = L < 4 ? __builtin_amdgcn_ubfe(x, (8 * L) & 31, 8) : __builtin_amdgcn_ubfe(tw3[1], 8 * r, 8);
+        v = digits4((x & 0x0F0F0F0Fu) << ((32 - 8 * L) & 31));
+        ok = L > 0;
+        if (L == 4 && tb - 0x30u < 10u) {  // 5 or more digits: bytes 4-7
+            const uint32_t y = __builtin_amdgcn_alignbyte(tw3[2], tw3[1], r);
+            const uint32_t nd2 = nondigit_bytes(y);
+            const uint32_t L2 = nd2 ? (uint32_t)__builtin_ctz(nd2) >> 3 : 4u;  // >= 1
+            tb = L2 < 4 ? __builtin_amdgcn_ubfe(y, (8 * L2) & 31, 8) : __builtin_amdgcn_ubfe(tw3[2], 8 * r, 8);
+            const uint32_t p10 = L2 == 1 ? 10u : L2 == 2 ? 100u : L2 == 3 ? 1000u : 10000u;
+            v = v * p10 + digits4((y & 0x0F0F0F0Fu) << ((32 - 8 * L2) & 31));
+            if (L2 == 4 && tb - 0x30u < 10u) {  // 9 or more: walked
+                v = parse_token_walk(t, nullptr, 0, ps, ok);
+                tb = 0x20u;
+            }
+        }
+        ok = ok && (tb == 0x20u || (tb < 14u && ((0x3600u >> tb) & 1u))) && v <= 65535u;
+    } else {  // the text's last bytes: walked
+        v = parse_token_walk(t, nullptr, 0, ps, ok);
+    }
+    return v;
+}
+
 // One chunk's global loads, issued together (see k_ppm_fast)
 struct FastLoads {
     uint4 v[kFastPieces];
@@ -429,8 +475,9 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
     constexpr int NW = kPpmThreads / 64, P = kFastPieces;
     // the chunk (' ' outside the body) + the next 16 bytes, staged for the
     // neighbouring pieces' bytes; after the scan the same LDS holds the token
-    // entries in text order (at most one token per two bytes)
-    __shared__ uint32_t sLds[kFastChunk / 2];
+    // entries in text order (at most one token per two bytes), shifted by the
+    // output's alignment (up to 3 slots) and padded to whole groups of four
+    __shared__ __attribute__((aligned(16))) uint32_t sLds[kFastChunk / 2 + 8];
     uint32_t* const sText = sLds;
     uint32_t* const sTok = sLds;
     static_assert(kFastChunk / 4 + 4 <= kFastChunk / 2, "the staged text fits the entry array");
@@ -533,15 +580,28 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         const uint32_t ntok = T0 + T1;
         const uint32_t rank[P] = {e01 & 0xFFFFu, T0 + (e01 >> 16)};
         const unsigned long long base = sBase;
+        // The token loop stores four samples per thread as one aligned vector store:
+        // the entries are shifted by `pad` slots so that entry group g (slots 4g..4g+3)
+        // covers one aligned 4-sample group of the output.  (A 16-bit output at an
+        // odd address is stored sample by sample, pad 0.)
+        Out* const ob = out + base;
+        const uintptr_t oaddr = reinterpret_cast<uintptr_t>(ob);
+        const bool vec = oaddr % sizeof(Out) == 0;
+        const uint32_t pad = vec ? (uint32_t)((oaddr & (4 * sizeof(Out) - 1)) / sizeof(Out)) : 0u;
+        const uint32_t ngroups = (ntok + pad + 3) >> 2;
+        // the slots outside [pad, pad + ntok) of the groups read as the token "0"
+        if (tid < (int)pad) sTok[tid] = 0x30u;
+        if (tid < (int)(4 * ngroups - pad - ntok)) sTok[pad + ntok + tid] = 0x30u;
         // compaction: at most two starts per word (a start follows whitespace).  A
         // token's entry is its first four bytes with everything from its terminating
         // whitespace on zeroed -- its digits, which the thread of the token combines --
         // or, for a token of four or more bytes, 0x80000000 | its chunk offset (its
-        // text is read back from global memory)
+        // text is read back from global memory).  Both are formed and one selected
+        // (no branch).
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             const uint32_t off = 16u * (uint32_t)(tid + kPpmThreads * q);
-            uint32_t r = rank[q];
+            uint32_t r = rank[q] + pad;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t m = st[q][k];
@@ -551,8 +611,10 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                     auto entry = [&](uint32_t a) {
                         const uint32_t x = __builtin_amdgcn_alignbyte(wn, w[q][k], a);
                         const uint32_t ws = __builtin_amdgcn_alignbyte(wsn, wsw, a);  // 0x80: whitespace byte
-                        const uint32_t keep = ((ws & (0u - ws)) >> 7) - 1u;           // the bytes before the first
-                        return ws ? x & keep : 0x80000000u | (off + 4 * k + a);
+                        // the bytes before the first whitespace byte (ws ^ (ws - 1) runs up to its bit 7)
+                        uint32_t e = x & ((ws ^ (ws - 1u)) >> 8);
+                        asm volatile("" : "+v"(e));  // (formed on every lane: a select, not a branch)
+                        return ws ? e : 0x80000000u | (off + 4 * k + a);
                     };
                     sTok[r] = entry((uint32_t)__builtin_ctz(m) >> 3);
                     if (m & (m - 1u)) sTok[r + 1] = entry((uint32_t)(31 - __clz((int)m)) >> 3);
@@ -561,51 +623,47 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
             }
         }
         __syncthreads();
-        // one thread per token: the entry's digits (the text of a token of four or
-        // more bytes is read back from global memory, its terminator checked there)
-        Out* const ob = out + base;
+        // one thread per group of four tokens: the entries' digits (the text of a
+        // token of four or more bytes is read back from global memory, its
+        // terminator checked there), stored as one vector where the group lies whole
+        // inside the image
         const uint32_t lim = base < nsamples ? (uint32_t)min((unsigned long long)ntok, nsamples - base) : 0u;
-        for (uint32_t i = (uint32_t)tid; i < ntok; i += kPpmThreads) {
-            const uint32_t e = sTok[i];
-            uint32_t v;
-            if (!(e & 0x80000000u)) {  // 1-3 digits: e's bytes past them are zero
-                const uint32_t L = (uint32_t)(32 - __clz((int)e) + 7) >> 3;
-                v = digits4((e & 0x0F0F0F0Fu) << (32 - 8 * L));
-            } else {  // four or more bytes (u16 samples, leading zeros)
-                const long long ps = c0 + (e & 0xFFFFu);
-                const long long pa = ps & ~3ll;
-                bool ok = true;
-                if (pa + 12 <= t.len) {
-                    uint32_t tw3[3];
+        for (uint32_t g = (uint32_t)tid; g < ngroups; g += kPpmThreads) {
+            const uint4 e4 = reinterpret_cast<const uint4*>(sTok)[g];
+            const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
+            uint32_t v[4];
 #pragma unroll
-                    for (int u = 0; u < 3; ++u) tw3[u] = *reinterpret_cast<const uint32_t*>(t.text + pa + 4 * u);
-                    const uint32_t r = (uint32_t)(ps & 3);
-                    const uint32_t x = __builtin_amdgcn_alignbyte(tw3[1], tw3[0], r);
-                    const uint32_t nd = nondigit_bytes(x);
-                    const uint32_t L = nd ? (uint32_t)__builtin_ctz(nd) >> 3 : 4u;
-                    uint32_t tb = L < 4 ? __builtin_amdgcn_ubfe(x, (8 * L) & 31, 8) : __builtin_amdgcn_ubfe(tw3[1], 8 * r, 8);
-                    v = digits4((x & 0x0F0F0F0Fu) << ((32 - 8 * L) & 31));
-                    ok = L > 0;
-                    if (L == 4 && tb - 0x30u < 10u) {  // 5 or more digits: bytes 4-7
-                        const uint32_t y = __builtin_amdgcn_alignbyte(tw3[2], tw3[1], r);
-                        const uint32_t nd2 = nondigit_bytes(y);
-                        const uint32_t L2 = nd2 ? (uint32_t)__builtin_ctz(nd2) >> 3 : 4u;  // >= 1
-                        tb = L2 < 4 ? __builtin_amdgcn_ubfe(y, (8 * L2) & 31, 8) : __builtin_amdgcn_ubfe(tw3[2], 8 * r, 8);
-                        const uint32_t p10 = L2 == 1 ? 10u : L2 == 2 ? 100u : L2 == 3 ? 1000u : 10000u;
-                        v = v * p10 + digits4((y & 0x0F0F0F0Fu) << ((32 - 8 * L2) & 31));
-                        if (L2 == 4 && tb - 0x30u < 10u) {  // 9 or more: walked
-                            v = parse_token_walk(t, nullptr, 0, ps, ok);
-                            tb = 0x20u;
-                        }
+            for (int j = 0; j < 4; ++j) v[j] = short_token(e[j]);
+            if ((e[0] | e[1] | e[2] | e[3]) & 0x80000000u) {  // four or more bytes (u16 samples, leading zeros)
+#pragma unroll 1
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t ej = j == 0 ? e[0] : j == 1 ? e[1] : j == 2 ? e[2] : e[3];
+                    if (ej & 0x80000000u) {
+                        bool ok;
+                        const uint32_t x = long_token(t, c0 + (ej & 0xFFFFu), ok);
+                        bad |= !ok;
+                        v[0] = j == 0 ? x : v[0];
+                        v[1] = j == 1 ? x : v[1];
+                        v[2] = j == 2 ? x : v[2];
+                        v[3] = j == 3 ? x : v[3];
                     }
-                    ok = ok && (tb == 0x20u || (tb < 14u && ((0x3600u >> tb) & 1u))) && v <= 65535u;
-                } else {  // the text's last bytes: walked
-                    v = parse_token_walk(t, nullptr, 0, ps, ok);
                 }
-                bad |= !ok;
             }
-            over |= v > maxval;
-            if (i < lim) ob[i] = (Out)(sizeof(Out) == 1 ? min(v, 255u) : min(v, 65535u));
+            over |= max(max(v[0], v[1]), max(v[2], v[3])) > maxval;
+            const int i0 = 4 * (int)g - (int)pad;  // the group's first token
+            constexpr uint32_t cap = sizeof(Out) == 1 ? 255u : 65535u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = min(v[j], cap);
+            if (vec && i0 >= 0 && (uint32_t)i0 + 4u <= lim) {
+                if (sizeof(Out) == 1)
+                    *reinterpret_cast<uint32_t*>(ob + i0) = v[0] | v[1] << 8 | v[2] << 16 | v[3] << 24;
+                else
+                    *reinterpret_cast<uint2*>(ob + i0) = make_uint2(v[0] | v[1] << 16, v[2] | v[3] << 16);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (i0 + j >= 0 && (uint32_t)(i0 + j) < lim) ob[i0 + j] = (Out)v[j];
+            }
         }
     }
     if (bad) reinterpret_cast<volatile uint32_t*>(&rep->bad)[0] = 1u;
