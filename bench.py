@@ -510,16 +510,17 @@ def kernel_roofline(prof, algo_bytes, frames_per_launch, pmc):
     return out
 
 
-def path_roofline(algo_bytes, achieved, step_s, pmc):
+def path_roofline(algo_bytes, achieved, step_s, pmc, launched):
     """the whole step against both ceilings: the HBM fraction of the
     step's algorithmic bytes, and the issue ceiling -- the VALU wave-instructions all
     kernels of a step issue (PMC, profiles/pmc_<config>.json) over the step time
-    against the measured 1.003 T wave-instructions/s (tools/pk_rate.hip)"""
+    against the measured 1.003 T wave-instructions/s (tools/pk_rate.hip).  `launched`:
+    the kernels the step ran (k_offsets only when k_emit did not fuse the offsets)"""
     out = {"algorithmic_bytes_per_step": round(algo_bytes), "achieved": round(achieved, 1),
            "frac": round(achieved / HBM_PEAK_GBS, 4), "valu_wave_insts": None, "salu_wave_insts": None,
            "valu_frac": None}
-    ks = {n: k for n, k in (pmc or {}).get("kernels", {}).items() if n in KERNELS.values()}  # the step's kernels
-    if len(ks) == len(KERNELS) and all(k.get("SQ_INSTS_VALU") is not None for k in ks.values()):
+    ks = {n: k for n, k in (pmc or {}).get("kernels", {}).items() if n in launched}  # the step's kernels
+    if launched and len(ks) == len(launched) and all(k.get("SQ_INSTS_VALU") is not None for k in ks.values()):
         valu = sum(k["SQ_INSTS_VALU"] for k in ks.values())
         out["valu_wave_insts"] = round(valu)
         out["valu_frac"] = round(valu / step_s / VALU_PEAK_PER_S, 4)
@@ -720,7 +721,7 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
                 "algorithmic_bytes_per_launch": round(algo_bytes),
                 "algorithmic_bytes_def": "SURVEY 8(d): 3 B/px RGB in + JPEG bytes out, per frame, x frames per launch",
                 "kernels": kern,
-                "path": path_roofline(algo_bytes, path_achieved, elapsed / args.steps, pmc),
+                "path": path_roofline(algo_bytes, path_achieved, elapsed / args.steps, pmc, set(kern)),
                 "pmc_source": f"profiles/pmc_{args.config}.json" if pmc else None,
             },
             "cpu_baseline": cpu,

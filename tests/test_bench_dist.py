@@ -226,3 +226,19 @@ def test_bench_inproc_group(monkeypatch):
         expect = n * 3840 * 2160 * 6 / (line["ms_per_step"] * 6 / 1e3) / 1e6
         assert line["value"] == pytest.approx(expect, rel=2e-3)
         assert log[-1] == ("close",)
+
+
+def test_path_roofline_over_the_launched_kernels():
+    """roofline.path's issue ceiling sums the PMC of the kernels the step launched:
+    with the chunk offsets fused into k_emit there is no k_offsets launch, and the
+    ceiling is still reported; a launched kernel without PMC leaves it null"""
+    import bench
+
+    pmc = {"kernels": {n: {"SQ_INSTS_VALU": 1e6, "SQ_INSTS_SALU": 5e5}
+                       for n in ("k_front", "k_hist", "k_tables", "k_emit", "k_stuffwrite", "k_ppm_fast")}}
+    fused = {"k_front", "k_hist", "k_tables", "k_emit", "k_stuffwrite"}
+    p = bench.path_roofline(30e6, 500.0, 50e-6, pmc, fused)
+    assert p["valu_wave_insts"] == 5_000_000 and p["salu_wave_insts"] == 2_500_000
+    assert p["valu_frac"] == round(5e6 / 50e-6 / bench.VALU_PEAK_PER_S, 4)
+    assert bench.path_roofline(30e6, 500.0, 50e-6, pmc, fused | {"k_offsets"})["valu_frac"] is None
+    assert bench.path_roofline(30e6, 500.0, 50e-6, None, fused)["valu_frac"] is None
