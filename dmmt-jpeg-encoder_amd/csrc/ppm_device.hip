@@ -43,7 +43,10 @@ constexpr int kPpmCarryThreads = 1024;
 // takes kCountChunks chunks per workgroup (4 pieces per thread)
 constexpr int kFastPieces = 2;
 constexpr int kFastChunk = 16 * kFastPieces * kPpmThreads;
-constexpr int kCountChunks = 2;
+#ifndef DMMT_COUNT_CHUNKS
+#define DMMT_COUNT_CHUNKS 2
+#endif
+constexpr int kCountChunks = DMMT_COUNT_CHUNKS;
 
 // Transition maps: entry state s = (in comment) << 1 | (last kept byte a token
 // byte); entry s occupies bits [16s, 16s + 16): exit state << 14 | tokens started.
@@ -409,14 +412,15 @@ __device__ __forceinline__ uint32_t digits4(uint32_t d) {
     return __umul24(a, 10u) + (d >> 24);
 }
 
-// A short token's entry (its 1-3 ASCII digits in bytes 0-2, the bytes past them
-// zero) -> its value.  The digits' weights are 100/10/1 shifted down by the bytes
-// the token lacks: an ASCII digit's top byte has two leading zeros, so the entry's
-// leading-zero count is 10, 18 or 26 for 3, 2 or 1 digits, and (clz + 22) mod 32 is
-// the shift 0, 8 or 16.
+// A short token's entry (its first four bytes: 1-3 ASCII digits, then its
+// terminating whitespace and whatever follows) -> its value.  The terminator is the
+// first byte below '0' (every whitespace byte is; any other such byte has made
+// k_ppm_count raise `bad`): shifting it and what follows out of the word's top
+// leaves the digits in bytes 4 - L .. 3, combined against 100/10/1.
 __device__ __forceinline__ uint32_t short_token(uint32_t e) {
-    const uint32_t sh = ((uint32_t)__builtin_clz(e) + 22u) & 31u;  // (no entry is zero)
-    return __builtin_amdgcn_udot4(e & 0x0F0F0F0Fu, 0x00010A64u >> sh, 0u, false);
+    const uint32_t lt = ~((e | 0x80808080u) - 0x30303030u) & 0x80808080u;  // 0x80: a byte below '0' (never 0)
+    const uint32_t y = e << ((39u - (uint32_t)__builtin_ctz(lt)) & 31u);   // terminator at 8L + 7: shift 32 - 8L
+    return __builtin_amdgcn_udot4(y & 0x0F0F0F0Fu, 0x010A6400u, 0u, false);
 }
 
 // A token of four or more bytes at text position ps (read back from global memory,
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         // a lane shuffle, or for a wave's lane 0 the staged byte (the byte before the
         // chunk for piece 0)
         static_assert(P == 2, "the per-piece counts are scanned as two 16-bit fields");
-        uint32_t st[P][4], sg[P][4], wnext[P], snext[P];
+        uint32_t st[P][4], sg[P][4], wnext[P];
         uint32_t n01 = 0;  // starts per piece, two 16-bit fields
 #pragma unroll
         for (int q = 0; q < P; ++q) {
@@ -553,7 +557,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                 prev = pb << 31;
             }
             if (lane == 63) wnext[q] = sText[4 * (p + 1)];
-            snext[q] = sig_bytes(wnext[q]);
             uint32_t nq = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -590,14 +593,12 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         const uint32_t pad = vec ? (uint32_t)((oaddr & (4 * sizeof(Out) - 1)) / sizeof(Out)) : 0u;
         const uint32_t ngroups = (ntok + pad + 3) >> 2;
         // the slots outside [pad, pad + ntok) of the groups read as the token "0"
-        if (tid < (int)pad) sTok[tid] = 0x30u;
-        if (tid < (int)(4 * ngroups - pad - ntok)) sTok[pad + ntok + tid] = 0x30u;
+        if (tid < (int)pad) sTok[tid] = 0x20202030u;
+        if (tid < (int)(4 * ngroups - pad - ntok)) sTok[pad + ntok + tid] = 0x20202030u;
         // compaction: at most two starts per word (a start follows whitespace).  A
-        // token's entry is its first four bytes with everything from its terminating
-        // whitespace on zeroed -- its digits, which the thread of the token combines --
-        // or, for a token of four or more bytes, 0x80000000 | its chunk offset (its
-        // text is read back from global memory).  Both are formed and one selected
-        // (no branch).
+        // token's entry is its first four bytes -- its digits and terminator, which the
+        // thread of the token combines -- or, for a token of four or more bytes,
+        // 0x80000000 | its chunk offset (its text is read back from global memory).
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             const uint32_t off = 16u * (uint32_t)(tid + kPpmThreads * q);
@@ -607,14 +608,11 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                 const uint32_t m = st[q][k];
                 if (m) {
                     const uint32_t wn = k < 3 ? w[q][k + 1] : wnext[q];
-                    const uint32_t wsw = ~sg[q][k] & 0x80808080u, wsn = ~(k < 3 ? sg[q][k + 1] : snext[q]) & 0x80808080u;
                     auto entry = [&](uint32_t a) {
                         const uint32_t x = __builtin_amdgcn_alignbyte(wn, w[q][k], a);
-                        const uint32_t ws = __builtin_amdgcn_alignbyte(wsn, wsw, a);  // 0x80: whitespace byte
-                        // the bytes before the first whitespace byte (ws ^ (ws - 1) runs up to its bit 7)
-                        uint32_t e = x & ((ws ^ (ws - 1u)) >> 8);
-                        asm volatile("" : "+v"(e));  // (formed on every lane: a select, not a branch)
-                        return ws ? e : 0x80000000u | (off + 4 * k + a);
+                        // no byte below '0' (whitespace) among the four: four or more bytes
+                        const bool lng = (((x | 0x80808080u) - 0x30303030u) & 0x80808080u) == 0x80808080u;
+                        return lng ? 0x80000000u | (off + 4 * k + a) : x;
                     };
                     sTok[r] = entry((uint32_t)__builtin_ctz(m) >> 3);
                     if (m & (m - 1u)) sTok[r + 1] = entry((uint32_t)(31 - __clz((int)m)) >> 3);
