@@ -592,6 +592,9 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         const bool vec = oaddr % sizeof(Out) == 0;
         const uint32_t pad = vec ? (uint32_t)((oaddr & (4 * sizeof(Out) - 1)) / sizeof(Out)) : 0u;
         const uint32_t ngroups = (ntok + pad + 3) >> 2;
+#if DMMT_PPM_ABL == 1  // study: loads, staging, starts and scan only
+        if (ntok < 1000000u) return;
+#endif
         // the slots outside [pad, pad + ntok) of the groups read as the token "0"
         if (tid < (int)pad) sTok[tid] = 0x20202030u;
         if (tid < (int)(4 * ngroups - pad - ntok)) sTok[pad + ntok + tid] = 0x20202030u;
@@ -626,6 +629,9 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         // terminator checked there), stored as one vector where the group lies whole
         // inside the image
         const uint32_t lim = base < nsamples ? (uint32_t)min((unsigned long long)ntok, nsamples - base) : 0u;
+#if DMMT_PPM_ABL == 2  // study: no token loop
+        if (ntok < 1000000u) return;
+#endif
         for (uint32_t g = (uint32_t)tid; g < ngroups; g += kPpmThreads) {
             const uint4 e4 = reinterpret_cast<const uint4*>(sTok)[g];
             const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};
