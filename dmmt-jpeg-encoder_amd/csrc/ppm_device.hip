@@ -508,7 +508,13 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
     uint32_t over = 0;
     FastLoads cur;
     const long long c = blockIdx.x;
+#if DMMT_PPM_PRIO  // study: a starting workgroup's loads ahead of the parsing waves
+    __builtin_amdgcn_s_setprio(3);
+#endif
     issue(c, cur);
+#if DMMT_PPM_PRIO == 1
+    __builtin_amdgcn_s_setprio(0);
+#endif
     {
         const long long c0 = c * kFastChunk;
         const long long row0 = (c / per) * per;
@@ -534,6 +540,9 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         for (int q = 0; q < P; ++q)
             reinterpret_cast<uint4*>(sText)[tid + kPpmThreads * q] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
         if (tid < 4) sText[kFastChunk / 4 + tid] = tw;
+#if DMMT_PPM_PRIO == 2  // (the study's second form: raised until the text is staged)
+        __builtin_amdgcn_s_setprio(0);
+#endif
         __syncthreads();
         // token starts per word; a piece's previous byte is the last of piece (q, t - 1):
         // a lane shuffle, or for a wave's lane 0 the staged byte (the byte before the
