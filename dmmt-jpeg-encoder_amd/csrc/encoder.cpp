@@ -96,6 +96,7 @@ struct dmmt_ctx {
     void* ppm_report = nullptr;  // host-mapped report of the comment-free P3 path (24 bytes)
     void* ppm_batch_reports = nullptr;  // the same, one per file of dmmt_convert_ppm_device_batch
     size_t ppm_batch_cap = 0;           // (files)
+    int ppm_batch_redone = -1;          // files the last batch redid on their own (diagnostic)
     // uploaded table state
     int lut_maxval = -1, lut_sb = -1;
     uint8_t q_cached[128];
@@ -280,9 +281,10 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
 
 // workspace + tables for one launch batch; every table pointer is valid on return
 int prepare(dmmt_ctx* c, const Geom& g, int nf, const dmmt_options* opt, int sb, hipStream_t st, Work* w,
-            int lane = 0, bool async = false) {
+            int lane = 0, bool async = false, int* status = nullptr) {
     int rc;
     if ((rc = ensure_work(c, g, nf, w, lane, async))) return rc;
+    if (status) w->status = status;  // (a per-file status area of dmmt_convert_ppm_device_batch)
     if ((rc = upload_tables(c, opt, g.maxval, sb, st))) return rc;
     w->norm_lut = (const float*)c->lut.p;
     w->qtab = (const float*)c->qtab.p;
@@ -385,10 +387,10 @@ void destroy_graphs(dmmt_ctx* c) {
 // Stage profiling needs per-kernel events, so it always launches directly.
 int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, int nf, const Geom& g,
                    const dmmt_options* opt, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st,
-                   int lane = 0, bool async = false) {
+                   int lane = 0, bool async = false, int* status = nullptr) {
     Work w;
     int rc;
-    if ((rc = prepare(c, g, nf, opt, sb, st, &w, lane, async))) return rc;
+    if ((rc = prepare(c, g, nf, opt, sb, st, &w, lane, async, status))) return rc;
     const int bits = opt->bits_per_channel;
     if (!c->use_graphs || c->profile)
         return enqueue_direct(c, d_rgb, frame_stride, sb, nf, g, w, bits, out, out_stride, out_len, st);
@@ -970,22 +972,26 @@ extern "C" int dmmt_convert_ppm_device_batch(dmmt_ctx* c, const dmmt_ppm_file* f
     // the bits this batch raises are its own
     for (Lane* L : c->lanes)
         if ((rc = collect_async(c, L))) return rc;
+    // per file, in host-mapped memory: the comment-free decode's report, then the
+    // status words of its speculative encode (raise_status), so that a file whose
+    // encode fails -- a comment's garbage samples above maxval, say -- sends only
+    // itself down the exact path, not every file of its lane
+    constexpr size_t kFileBytes = kPpmReportBytes + kStatusWords * sizeof(int);
     if ((size_t)n > c->ppm_batch_cap) {
         if (c->ppm_batch_reports) (void)hipHostFree(c->ppm_batch_reports);
         c->ppm_batch_reports = nullptr;
         c->ppm_batch_cap = 0;
-        HIP_TRY(hipHostMalloc(&c->ppm_batch_reports, (size_t)n * kPpmReportBytes,
+        HIP_TRY(hipHostMalloc(&c->ppm_batch_reports, (size_t)n * kFileBytes,
                               hipHostMallocMapped | hipHostMallocCoherent));
         c->ppm_batch_cap = (size_t)n;
     }
     uint8_t* const reps = (uint8_t*)c->ppm_batch_reports;
-    memset(reps, 0, (size_t)n * kPpmReportBytes);  // (no kernel is writing them: the lanes are idle)
+    memset(reps, 0, (size_t)n * kFileBytes);  // (no kernel is writing them: the lanes are idle)
     uint8_t* dreps = nullptr;
     HIP_TRY(hipHostGetDevicePointer((void**)&dreps, c->ppm_batch_reports, 0));
     // state per file: 0 done (codes[i] final), 1 speculative fast-path P3 (report i), 2
     // speculative P6, 3 redo on its own
     std::vector<uint8_t> state((size_t)n, 0);
-    std::vector<int> lane_of((size_t)n, 0);
     for (int i = 0; i < n; ++i) codes[i] = DMMT_OK;
     for (int i = 0; i < n; ++i) {
         const dmmt_ppm_file& f = files[i];
@@ -1010,7 +1016,6 @@ extern "C" int dmmt_convert_ppm_device_batch(dmmt_ctx* c, const dmmt_ppm_file* f
         const int lane = c->nlanes > 1 ? (int)(c->next_lane++ % (unsigned)c->nlanes) : 0;
         Lane* L = c->lanes[lane];
         hipStream_t st = L->stream;
-        lane_of[i] = lane;
         if ((rc = ensure(L->ppm_rgb, ns * (size_t)sb))) return rc;
         if (h.binary) {
             HIP_TRY(launch_ppm_p6(f.d_text + h.body_offset, L->ppm_rgb.p, sb, ns, h.maxval, nullptr, st));
@@ -1020,35 +1025,52 @@ extern "C" int dmmt_convert_ppm_device_batch(dmmt_ctx* c, const dmmt_ppm_file* f
             if ((rc = ensure(L->ppm_counts, ppm_counts_capacity((long long)nch) * 4))) return rc;
             if ((rc = ensure(L->ppm_rowbase, std::max<size_t>(nch, 1024) * 8))) return rc;
             HIP_TRY(launch_ppm_p3_fast(f.d_text, h.body_offset, f.len, (uint32_t*)L->ppm_counts.p,
-                                       (unsigned long long*)L->ppm_rowbase.p, dreps + (size_t)i * kPpmReportBytes,
+                                       (unsigned long long*)L->ppm_rowbase.p, dreps + (size_t)i * kFileBytes,
                                        L->ppm_rgb.p, sb, ns, h.maxval, st));
             state[i] = 1;
         }
         // encoded at once, on the assumption that the decode succeeds (checked below)
+        int* const fstatus = (int*)(dreps + (size_t)i * kFileBytes + kPpmReportBytes);
         if ((rc = enqueue_encode(c, L->ppm_rgb.p, ns * (size_t)sb, sb, 1, g, opt, f.d_out, f.out_capacity,
-                                 f.d_out_len, st, lane, true))) return rc;
+                                 f.d_out_len, st, lane, true, fstatus))) return rc;
     }
-    std::vector<int> lane_bits(c->lanes.size(), 0);
-    for (size_t l = 0; l < c->lanes.size(); ++l)
-        if ((rc = read_status(c->lanes[l], kStatusAsync, c->lanes[l]->stream, &lane_bits[l]))) return rc;
+    if ((rc = sync_lanes(c))) return rc;
     for (int i = 0; i < n; ++i) {
         if (state[i] == 0 || state[i] == 3) continue;
-        bool ok = lane_bits[lane_of[i]] == 0;  // an encode error on the lane: its files are redone
+        const uint8_t* fb = reps + (size_t)i * kFileBytes;
+        const volatile int* fs = (const volatile int*)(fb + kPpmReportBytes);
+        bool ok = true;  // the file's own encode raised nothing
+        for (int k = 0; k < kStatusWords; ++k) ok = ok && fs[k] == 0;
         if (state[i] == 1) {
-            const volatile uint32_t* r = (const volatile uint32_t*)(reps + (size_t)i * kPpmReportBytes);
+            const volatile uint32_t* r = (const volatile uint32_t*)fb;
             const unsigned long long tokens = (unsigned long long)r[4] | ((unsigned long long)r[5] << 32);
             const unsigned long long ns = (unsigned long long)files[i].header.width * files[i].header.height * 3ull;
             ok = ok && r[1] == 0u && r[2] == 0u && tokens == ns;  // else: the general path, or an error
         }
         state[i] = ok ? 0 : 3;
     }
-    // the files the pipeline could not settle, one at a time with the exact error
-    int first = DMMT_OK;
+    // the files the pipeline could not settle, one at a time with the exact error;
+    // the payload kept for dmmt_last_error_detail is the one of the file whose code
+    // is returned (the first that failed), whatever the files redone after it set
+    int first = DMMT_OK, first_detail = 0;
+    c->ppm_batch_redone = 0;
     for (int i = 0; i < n; ++i) {
-        if (state[i] == 3) codes[i] = convert_one_device(c, files[i], opt);
-        if (codes[i] != DMMT_OK && first == DMMT_OK) first = codes[i];
+        if (state[i] == 3) {
+            codes[i] = convert_one_device(c, files[i], opt);
+            ++c->ppm_batch_redone;
+        }
+        if (codes[i] != DMMT_OK && first == DMMT_OK) {
+            first = codes[i];
+            first_detail = state[i] == 3 ? dmmt_last_error_detail() : 0;
+        }
     }
+    dmmt::error_detail(first, first_detail);
     return first;
+}
+
+extern "C" int dmmt_ctx_batch_redone(dmmt_ctx* c) {
+    c = primary(c);
+    return c ? c->ppm_batch_redone : -1;
 }
 
 // convert_ppm_to_jpeg over several GPUs: the samples parsed on the host

@@ -34,6 +34,7 @@
 #include "device_common.hpp"
 #include "jpeg_common.hpp"
 #include "kernels.hpp"
+#include "slot_copy.hpp"
 
 namespace dmmt {
 
@@ -53,6 +54,19 @@ constexpr int kEmitOcc = kChunkBlocks == 256 ? 7 : 3;  // workgroups per CU
 constexpr int kEmitWords = 4 * kChunkBlocks;
 // Bytes per pass of k_stuffwrite (16 per thread).
 constexpr int kStuffPass = 4096;
+// The fused offsets' hand-off (k_emit): 1 = release / acquire ordering under the
+// HIP memory model; 0 = the round-4 form (relaxed atomics after an s_waitcnt
+// vmcnt(0), correct by the gfx950 ISA argument of DESIGN.md 3; measurement builds)
+#ifndef DMMT_ARRIVE_FORMAL
+#define DMMT_ARRIVE_FORMAL 1
+#endif
+#if DMMT_ARRIVE_FORMAL
+#define DMMT_ARRIVE_ORDER __ATOMIC_RELEASE
+#define DMMT_ARRIVE_TOP_ORDER __ATOMIC_ACQ_REL
+#else
+#define DMMT_ARRIVE_ORDER __ATOMIC_RELAXED
+#define DMMT_ARRIVE_TOP_ORDER __ATOMIC_RELAXED
+#endif
 #ifndef DMMT_EMIT_PRIO
 #define DMMT_EMIT_PRIO 1  // k_emit's wave priorities by walk length (0: off, study builds)
 #endif
@@ -126,12 +140,9 @@ __device__ __forceinline__ int coef_at(const BlockCoef& b, int k) {
 // a wave's first block, differently from run to run; the round-3 study
 // (profiles/r03_kemit_fault_study.md) traced it to code generation -- exact at -O1
 // and without the SDWA peephole, unchanged by waits after every instruction -- not
-// to a race in this kernel.  The current tree is exact either way
-// (DMMT_WALK_COLUMN_MAJOR); tests/test_gpu_regressions.py guards the shape.)
+// to a race in this kernel.  The study switch is profiles/r05_study_variants.patch;
+// tests/test_gpu_regressions.py guards the shape.)
 __device__ __forceinline__ void zigzag_in_registers(BlockCoef& b) {
-#ifdef DMMT_WALK_COLUMN_MAJOR
-    return;
-#endif
     uint32_t z[32];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
@@ -161,11 +172,7 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
 #pragma unroll
     for (int k = 1; k < 64; ++k) {
         if (k > kmax) continue;  // (wave-uniform) every later position is zero in every lane
-#ifdef DMMT_WALK_COLUMN_MAJOR  // study build: the walk straight over the column-major block
-        const int v = coef_at(b, coef_pos(k));
-#else
         const int v = coef_at(b, k);
-#endif
         if (v != 0) {
             const int r16 = 16 * k - l16;
             for (int r = r16 >> 8; r > 0; --r) sink(z.x, (int)z.y);
@@ -226,11 +233,10 @@ struct WindowSink {
 
 // Private block slots of k_emit: every thread writes its block's bits MSB-first
 // from bit 0 of its own slot (no sharing, plain stores), word i of thread t at
-// sSlot[i * 256 + t] (consecutive threads, consecutive banks).  A block that needs
-// more than kSlotWords words (384 bits) sets `over`; the chunk then takes the
-// re-walk path.  Small slots and window keep 7 workgroups resident per CU.
-constexpr int kSlotWords = 12;
-
+// sSlot[i * kEmitThreads + t] (consecutive threads, consecutive banks).  A block
+// that needs more than kSlotWords words (384 bits, slot_copy.hpp) sets `over`; the
+// chunk then takes the re-walk path.  Small slots and window keep 7 workgroups
+// resident per CU.
 struct SlotSink {
     uint32_t* slot;  // &sSlot[tid]
     unsigned long long acc;
@@ -246,77 +252,16 @@ struct SlotSink {
             ++wi;
         }
     }
+    // (the bits after the block in its last word are zero; the slot's later words
+    // are stale -- read_slot masks them)
     __device__ __forceinline__ uint32_t finish() {
         if (nacc > 0 && wi < kSlotWords) slot[wi * kEmitThreads] = (uint32_t)(acc << (32 - nacc));
         return (uint32_t)wi * 32u + (uint32_t)nacc;
     }
 };
 
-// The walker's copy of its slot (sSlot column tid, nbits bits) into the window
-// image of words [w0, w0 + wn] at chunk bit s0: destination word d gets
-// ({slot[k-1], slot[k]} >> sh) for k = d - d0; the first and last word are shared
-// with the neighbouring blocks (ORed), the rest are this block's alone
-__device__ __forceinline__ void copy_slot(const uint32_t* __restrict__ sSlot, int tid, uint32_t s0, uint32_t nbits,
-                                          uint32_t* sW, int w0, int wn) {
-    if (!nbits || s0 >= (uint32_t)(w0 + wn + 1) * 32u || s0 + nbits <= (uint32_t)w0 * 32u) return;
-    const int sh = (int)(s0 & 31);
-    const int d0 = (int)(s0 >> 5), d1 = (int)((s0 + nbits - 1) >> 5);
-    const int nsw = (int)((nbits + 31) >> 5);
-    const int da = max(d0, w0), db = min(d1, w0 + wn);
-    uint32_t prev = da > d0 ? sSlot[(da - d0 - 1) * kEmitThreads + tid] : 0u;
-    for (int d = da; d <= db; ++d) {
-        const int k = d - d0;
-        const uint32_t cur = k < nsw ? sSlot[k * kEmitThreads + tid] : 0u;
-        const uint32_t v = __builtin_amdgcn_alignbit(prev, cur, (uint32_t)sh);
-        prev = cur;
-        if (d == d0 || d == d1)
-            atomicOr(&sW[d - w0], v);
-        else
-            sW[d - w0] = v;
-    }
-}
-
-// The same copy, unrolled and without a window clear (the product path): the
-// thread of block t (stream order: its offset is its own scan value, its walker
-// the rank it drew in the sort) reads all kSlotWords words of the walker's slot at
-// once -- no barrier is needed between the scan and the copy -- then
-//  copy_owned  (phase 1) stores, plainly, every window word whose first bit lies
-//              in its block: word d0 + k = {slot[k-1], slot[k]} >> sh (slot[-1] =
-//              0) for k >= 1, and k = 0 too when the block starts word-aligned --
-//              each window word has exactly one such block, so no word needs
-//              clearing and none is written twice;
-//  copy_head   (phase 2, after a barrier) ORs the block's first 32 - sh bits into
-//              word d0, which an earlier block owns (a word can collect the heads
-//              of several short blocks).
-// The looped version waited out one LDS read per copied word.
-struct SlotWords {
-    uint32_t w[kSlotWords];
-};
-__device__ __forceinline__ void read_slot(const uint32_t* __restrict__ sSlot, int tid, uint32_t nbits, SlotWords& W) {
-    const int nsw = (int)((nbits + 31) >> 5);
-#pragma unroll
-    for (int k = 0; k < kSlotWords; ++k) W.w[k] = sSlot[k * kEmitThreads + tid];
-#pragma unroll
-    for (int k = 0; k < kSlotWords; ++k) W.w[k] = k < nsw ? W.w[k] : 0u;  // words past the block: stale
-}
-__device__ __forceinline__ void copy_owned(const SlotWords& W, uint32_t s0, uint32_t nbits, uint32_t* sW, int w0,
-                                           int wn) {
-    if (!nbits) return;
-    const uint32_t sh = s0 & 31u;
-    const int d0 = (int)(s0 >> 5), d1 = (int)((s0 + nbits - 1) >> 5);
-#pragma unroll
-    for (int k = 0; k <= kSlotWords; ++k) {
-        const int d = d0 + k;
-        const uint32_t v = __builtin_amdgcn_alignbit(k ? W.w[k - 1] : 0u, k < kSlotWords ? W.w[k] : 0u, sh);
-        if (d <= d1 && (k || !sh) && (unsigned)(d - w0) <= (unsigned)wn) sW[d - w0] = v;
-    }
-}
-__device__ __forceinline__ void copy_head(const SlotWords& W, uint32_t s0, uint32_t nbits, uint32_t* sW, int w0,
-                                          int wn) {
-    const uint32_t sh = s0 & 31u;
-    const int d0 = (int)(s0 >> 5);
-    if (nbits && sh && (unsigned)(d0 - w0) <= (unsigned)wn) atomicOr(&sW[d0 - w0], W.w[0] >> sh);
-}
+// The slot's copy into the window (read_slot, copy_owned, copy_head) is in
+// slot_copy.hpp, shared with its host unit check.
 
 // 16 bits of an MSB-first word stream starting at bit p (p & 31 taken; words a, b
 // hold bits from (p & ~31))
@@ -361,9 +306,6 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     __shared__ unsigned long long sOffV[kEmitWaves + 1];  // fused offsets: the scans' wave totals, the carry
     __shared__ int sOffF[kEmitWaves];
     __shared__ uint32_t sLast;
-#ifdef DMMT_EMIT_COPY_LOOP
-    __shared__ uint32_t sStart[kEmitThreads];  // bit offset of block t in the chunk
-#endif
     using OrderT = std::conditional_t<(kEmitThreads > 256), uint16_t, uint8_t>;
     uint32_t* const sBits = sW;                                                      // bit count of block t
     OrderT* const sOrder = reinterpret_cast<OrderT*>(sW + kEmitThreads);               // block walked by thread u
@@ -426,10 +368,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     }
     __syncthreads();
     DMMT_TRACE(0);
-#ifdef DMMT_EMIT_COPY_LOOP
-    int pw = 0;          // the block this thread walks
-#endif
-    uint32_t wbits = 0;  // and its bits
+    uint32_t wbits = 0;  // the bits of the block this thread walks
     bool slot_over = false;
     {
 #if DMMT_EMIT_PRIO
@@ -444,9 +383,6 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         // one walk: the block's bits into this thread's private slot, and its bit count
         if (valid) {
             const int p = sOrder[tid];
-#ifdef DMMT_EMIT_COPY_LOOP
-            pw = p;
-#endif
             const long long ep = (long long)frame * g.bpf + el0 + p;
             BlockCoef b;
             load_block(coef + ep * 64, b);
@@ -458,18 +394,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             // the wave's walk stops after the last position any of its blocks uses
             const int kmax = __builtin_amdgcn_readfirstlane((int)sKey[min(64 * wave + 63, nb - 1)]);
             SlotSink ss{sSlot + tid, 0ull, 0, 0};
-#ifdef DMMT_ABL_NOWALK  // timing bound: no symbol walk, ~5.5 bits per zigzag position up to lastnz
-            {
-                const int np = (int)sKey[tid] / 2 + 1;
-                uint32_t acc = b.w[0] ^ (uint32_t)dp;
-                for (int j = 0; j < np; ++j) acc ^= b.w[j & 31];
-                for (int j = 0; j < np; ++j) ss(acc & 0x7FFu, 11);
-                (void)kmax;
-                (void)lum;
-            }
-#else
             walk_block(b, dp, sTab + 512 + (lum ? 0 : 16), sTab + (lum ? 0 : 256), ss, kmax);
-#endif
             wbits = ss.finish();
             slot_over = wbits > (uint32_t)kSlotWords * 32u;
             sBits[p] = wbits;
@@ -497,19 +422,15 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     }
     DMMT_TRACE(1);
 
-#ifdef DMMT_EMIT_COPY_LOOP
-    sStart[tid] = start;  // (read by the block's walker after the window clear's barrier)
-#endif
     uint32_t* slot = stage + cid * (size_t)kChunkWordsCap;
     const int nw = (int)((total + 31) >> 5);
     const int we1 = total >= 16 ? (int)((total - 16) >> 5) : 0;  // word holding bit total-16
     uint32_t ff[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int w0 = 0; w0 < nw; w0 += kEmitWords) {  // uniform; one window unless the chunk is huge
         const int wn = min(kEmitWords, nw - w0);
-#ifndef DMMT_EMIT_COPY_LOOP
         if (!over) {  // (uniform) block tid's bits from its walker's slot (column `mine`)
             SlotWords sw;
-            read_slot(sSlot, mine, bits, sw);
+            read_slot<kEmitThreads>(sSlot, mine, bits, sw);
             if (tid == 0 && w0 + wn >= nw) sW[wn] = 0u;  // past the stream: no block owns it
             copy_owned(sw, start, bits, sW, w0, wn);
             __syncthreads();
@@ -519,15 +440,6 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             __syncthreads();
         }
         if (over && bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
-#else
-        for (int i = tid; i <= wn; i += kEmitThreads) sW[i] = 0u;  // + the next window's first word
-        __syncthreads();
-        if (!over) {
-            // the walking thread shifts its own slot into place (the wave's slot reads
-            // are consecutive words)
-            copy_slot(sSlot, tid, wbits ? sStart[pw] : 0u, wbits, sW, w0, wn);
-        } else if (bits && start < (uint32_t)(w0 + wn + 1) * 32u && start + bits > (uint32_t)w0 * 32u) {
-#endif
             {
                 // the block again (L2 / MALL) and a second walk straight into the
                 // window: holding it in registers across the scan would halve the
@@ -575,43 +487,58 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         }
     }
     __syncthreads();
-    // the chunk's summary, stored write-through (agent scope): the frame's last
-    // workgroup reads it when the offsets are fused
-    if (tid < 8) __hip_atomic_store(chunk_ff + cid * 8 + tid, sFF[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // The chunk's summary (its bits, edge bits and eight 0xFF counts), stored by
+    // thread 0 as agent-scope atomics: the frame's last workgroup reads it when the
+    // offsets are fused.
     if (tid == 0) {
-        __hip_atomic_store(chunk_bits + cid, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t first16 = sEdge[0] >> 16;
         uint32_t last16;
         if (total >= 16)
             last16 = bits16_at(sEdge[1], sEdge[2], (int)(total - 16));
         else
             last16 = total ? sEdge[0] >> (32 - total) : 0u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            __hip_atomic_store(chunk_ff + cid * 8 + r, sFF[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(chunk_bits + cid, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(chunk_edge + cid, (first16 << 16) | last16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (fuse) {  // (uniform) count this workgroup in once its summary has reached memory
         // Two levels of counters, each on its own 128-byte line: chunk c counts into
         // group c mod kArriveGroups, the last of a group into the frame's top
         // counter (atomics on one address serialise: 1519 on a single counter cost
-        // ~18 us); every counter is reset by its last arriver
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        // ~18 us); every counter is reset by its last arriver.
+        // Ordering (HIP / C++ memory model, agent scope): thread 0 stored the
+        // summary and publishes it with a RELEASE increment of its group counter;
+        // the group's last arriver increments the top counter ACQ_REL (it acquires
+        // the group's releases and releases them on, a release sequence); the
+        // frame's last arriver thus happens-after every summary store, and its
+        // threads take an agent-scope ACQUIRE fence after the barrier that hands
+        // them the verdict before their agent-scope loads of the summaries.
         if (tid == 0) {
             uint32_t* const fa = arrive + (size_t)frame * kArriveWords;
             const int grp = (int)(chunk % kArriveGroups);
             const int ngrp = min(g.nch, kArriveGroups);
             const uint32_t in_grp = (uint32_t)((g.nch - grp + kArriveGroups - 1) / kArriveGroups);
             bool last = false;
-            if (__hip_atomic_fetch_add(fa + grp * kArriveStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+#if !DMMT_ARRIVE_FORMAL
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the summary stores have completed (sc1: past L2)
+#endif
+            if (__hip_atomic_fetch_add(fa + grp * kArriveStride, 1u, DMMT_ARRIVE_ORDER, __HIP_MEMORY_SCOPE_AGENT) ==
                 in_grp - 1u) {
                 __hip_atomic_store(fa + grp * kArriveStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 uint32_t* const top = fa + kArriveGroups * kArriveStride;
-                last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)ngrp - 1u;
+                last = __hip_atomic_fetch_add(top, 1u, DMMT_ARRIVE_TOP_ORDER, __HIP_MEMORY_SCOPE_AGENT) ==
+                       (uint32_t)ngrp - 1u;
                 if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             sLast = last;
         }
         __syncthreads();
         if (sLast) {  // every other chunk of the frame is done: its offsets
+#if DMMT_ARRIVE_FORMAL
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
             const size_t fb = (size_t)frame * g.nch;
             fused_offsets(chunk_bits + fb, chunk_ff + fb * 8, chunk_edge + fb, g, chunk_bit0 + fb, chunk_out + fb,
                           total_out + frame, sOffV, sOffF);

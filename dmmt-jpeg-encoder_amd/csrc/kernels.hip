@@ -636,12 +636,6 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
         // kk is r16 / 16 with r16 = 16 * kk - l16, (run & 15) << 4 = r16 & 0xF0
         int l16 = 16;
         uint32_t zrl = 0;
-#ifdef DMMT_HIST_ABL
-        uint32_t abl = 0;
-#endif
-#ifdef DMMT_ABL_TOKW
-        uint32_t ntokw = 0;
-#endif
 #pragma unroll
         for (int kk = 1; kk < 64; ++kk) {
             const int v = (kk & 1) ? ((int)b.w[kk >> 1] >> 16) : (int)(int16_t)(b.w[kk >> 1] & 0xFFFFu);
@@ -649,22 +643,11 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
                 if (CHECK && v == -32768) bad |= 4;
                 const int r16 = 16 * kk - l16;
                 zrl += (uint32_t)(r16 >> 8);
-#ifdef DMMT_ABL_TOKW  // timing bound: a 32-bit symbol token stored per non-zero (over the block itself)
-                reinterpret_cast<uint32_t*>(const_cast<int16_t*>(coef))[e * 32 + 8 + (ntokw++ & 15)] =
-                    ((uint32_t)(r16 >> 8) << 24) | ((uint32_t)((r16 & 0xF0) | category_fast(v)) << 16) | ((uint32_t)v & 0xFFFFu);
-#endif
-#ifdef DMMT_HIST_ABL  // timing study: the walk's histogram atomics replaced by a register XOR
-                abl ^= (uint32_t)((r16 & 0xF0) | category_fast(v)) << (kk & 15);
-#else
                 atomicAdd(&h[(r16 & 0xF0) | category_fast(v)], 1u);
-#endif
                 l16 = 16 * kk + 16;
             }
         }
         if (zrl) atomicAdd(&h[0xF0], zrl);
-#ifdef DMMT_HIST_ABL
-        if (abl == 0x7FFFFFFFu) h[1] = abl;  // (keeps the XOR)
-#endif
         if (l16 < 16 * 64) atomicAdd(&h[0], 1u);  // EOB
         lastnz[e] = (uint8_t)((l16 >> 4) - 1);      // 0: no non-zero AC coefficient
         {

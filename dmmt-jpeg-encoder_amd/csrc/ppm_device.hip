@@ -9,13 +9,16 @@
 // an optional '+', then decimal digits, value <= 65535).
 //
 // Two paths:
-//  comment-free bodies (no '#' after the header: every P3 writer's output), 16 KB
-//  chunks, 64 bytes per thread, classified by SWAR word arithmetic --
+//  comment-free bodies (no '#' after the header: every P3 writer's output), 8 KB
+//  chunks, 32 bytes per thread (two 16-byte pieces), classified by SWAR word
+//  arithmetic --
 //   k_ppm_count  every chunk's token count (a token starts at each token byte
-//                after whitespace); reports a '#' anywhere
+//                after whitespace), two chunks per workgroup; reports a token
+//                byte that is not a digit ('#' among them)
 //   k_ppm_rows   one workgroup: exclusive sums of the counts over 1024 rows
-//   k_ppm_fast   every chunk: its tokens parsed token by token (SWAR digits),
-//                staged in LDS in token order, stored coalesced
+//   k_ppm_fast   every chunk: its token starts compacted into LDS entries in
+//                token order, then one thread per four tokens (v_dot4 digits),
+//                one vector store per four samples
 //  The host reads the path's report (host-mapped memory, no copy) after it; a '#'
 //  sends the body down the general path, which a body shorter than 96 bytes takes
 //  from the start -- 4 KB chunks, 16 bytes per thread:
@@ -43,10 +46,7 @@ constexpr int kPpmCarryThreads = 1024;
 // takes kCountChunks chunks per workgroup (4 pieces per thread)
 constexpr int kFastPieces = 2;
 constexpr int kFastChunk = 16 * kFastPieces * kPpmThreads;
-#ifndef DMMT_COUNT_CHUNKS
-#define DMMT_COUNT_CHUNKS 2
-#endif
-constexpr int kCountChunks = DMMT_COUNT_CHUNKS;
+constexpr int kCountChunks = 2;  // (1 and 4 measured slower)
 
 // Transition maps: entry state s = (in comment) << 1 | (last kept byte a token
 // byte); entry s occupies bits [16s, 16s + 16): exit state << 14 | tokens started.
@@ -202,9 +202,9 @@ struct PpmText {
 
 // ---------------------------------------------------------------- comment-free path
 // Bodies whose tokens are all plain digit strings (every P3 writer's output) take
-// two passes over 16 KB chunks, the text loaded in coalesced 16-byte pieces
-// (piece p of a chunk = bytes [16p, 16p + 16); thread t holds pieces t, t + 256,
-// t + 512, t + 768):
+// two passes over 8 KB chunks, the text loaded in coalesced 16-byte pieces
+// (piece p of a chunk = bytes [16p, 16p + 16); thread t holds pieces t and
+// t + 256):
 //  k_ppm_count   each chunk's token count: a token starts at every non-whitespace
 //                byte whose previous byte is whitespace (or lies before the body)
 //  k_ppm_rows    one workgroup: exclusive sums of the counts over 1024 rows of chunks
@@ -508,13 +508,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
     uint32_t over = 0;
     FastLoads cur;
     const long long c = blockIdx.x;
-#if DMMT_PPM_PRIO  // study: a starting workgroup's loads ahead of the parsing waves
-    __builtin_amdgcn_s_setprio(3);
-#endif
     issue(c, cur);
-#if DMMT_PPM_PRIO == 1
-    __builtin_amdgcn_s_setprio(0);
-#endif
     {
         const long long c0 = c * kFastChunk;
         const long long row0 = (c / per) * per;
@@ -540,9 +534,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         for (int q = 0; q < P; ++q)
             reinterpret_cast<uint4*>(sText)[tid + kPpmThreads * q] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
         if (tid < 4) sText[kFastChunk / 4 + tid] = tw;
-#if DMMT_PPM_PRIO == 2  // (the study's second form: raised until the text is staged)
-        __builtin_amdgcn_s_setprio(0);
-#endif
         __syncthreads();
         // token starts per word; a piece's previous byte is the last of piece (q, t - 1):
         // a lane shuffle, or for a wave's lane 0 the staged byte (the byte before the
@@ -601,9 +592,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         const bool vec = oaddr % sizeof(Out) == 0;
         const uint32_t pad = vec ? (uint32_t)((oaddr & (4 * sizeof(Out) - 1)) / sizeof(Out)) : 0u;
         const uint32_t ngroups = (ntok + pad + 3) >> 2;
-#if DMMT_PPM_ABL == 1  // study: loads, staging, starts and scan only
-        if (ntok < 1000000u) return;
-#endif
         // the slots outside [pad, pad + ntok) of the groups read as the token "0"
         if (tid < (int)pad) sTok[tid] = 0x20202030u;
         if (tid < (int)(4 * ngroups - pad - ntok)) sTok[pad + ntok + tid] = 0x20202030u;
@@ -638,9 +626,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         // terminator checked there), stored as one vector where the group lies whole
         // inside the image
         const uint32_t lim = base < nsamples ? (uint32_t)min((unsigned long long)ntok, nsamples - base) : 0u;
-#if DMMT_PPM_ABL == 2  // study: no token loop
-        if (ntok < 1000000u) return;
-#endif
         for (uint32_t g = (uint32_t)tid; g < ngroups; g += kPpmThreads) {
             const uint4 e4 = reinterpret_cast<const uint4*>(sTok)[g];
             const uint32_t e[4] = {e4.x, e4.y, e4.z, e4.w};

@@ -101,6 +101,7 @@ def lib():
     L.dmmt_parse_ppm_header.argtypes = [vp, sz, P(DmmtPpmHeader)]
     L.dmmt_decode_ppm_device.argtypes = [vp, vp, sz, P(DmmtPpmHeader), vp, vp]
     L.dmmt_convert_ppm_device_batch.argtypes = [vp, P(DmmtPpmFile), i32, P(DmmtOptions), P(i32)]
+    L.dmmt_ctx_batch_redone.argtypes = [vp]
     L.dmmt_free.argtypes = [vp]
     L.dmmt_free.restype = None
     L.dmmt_strerror.argtypes = [ctypes.c_int]
@@ -516,6 +517,10 @@ class Encoder:
         if check:
             _check(rc, "convert_ppm_device_batch")
         return [codes[i] for i in range(n)]
+
+    def batch_redone(self) -> int:
+        """files the last convert_ppm_device_batch redid on their own (diagnostic)"""
+        return lib().dmmt_ctx_batch_redone(self._ctx)
 
     def read_ppm_device(self, data: bytes) -> Image:
         """PPMImageReader::read_image with the body decoded on the GPU: header on the

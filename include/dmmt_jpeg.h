@@ -294,10 +294,12 @@ int dmmt_convert_ppm_to_jpeg(dmmt_ctx* ctx, const char* input_path, const char* 
  * synchronisation between files: a P3 body is decoded on the comment-free path on the
  * assumption that it has no '#' and no error, and encoded at once; its report is checked
  * after the batch, and a file whose body needs the general path (a comment, a '+' sign),
- * or that fails, is redone on its own.  codes[i] receives file i's result: the code
- * dmmt_decode_ppm_device and then the encode would return for it (a failed file's size is
- * 0).  Returns the first non-zero code, DMMT_OK when every file succeeded; synchronised
- * before returning.  dmmt_last_error_detail: the payload of the last file that failed. */
+ * or that fails (its own decode report or its own encode's error words), is redone on its
+ * own.  codes[i] receives file i's result: the code dmmt_decode_ppm_device and then the
+ * encode would return for it (a failed file's size is 0).  Returns the first non-zero code,
+ * DMMT_OK when every file succeeded; synchronised before returning.
+ * dmmt_last_error_detail / dmmt_last_error_message: the payload of the file whose code is
+ * returned (the first that failed). */
 typedef struct {
     const uint8_t* d_text;   /* the whole file in device memory */
     size_t len;
@@ -308,6 +310,9 @@ typedef struct {
 } dmmt_ppm_file;
 int dmmt_convert_ppm_device_batch(dmmt_ctx* ctx, const dmmt_ppm_file* files, int32_t n, const dmmt_options* opt,
                                   int32_t* codes);
+/* Diagnostic: how many files the context's last dmmt_convert_ppm_device_batch redid on their
+ * own (a '#' or '+' in the text, or a failure); -1 before the first batch. */
+int dmmt_ctx_batch_redone(dmmt_ctx* ctx);
 /* The payload the reference's Error variant carries (error.rs:3-22), for the last error a PPM
  * entry point (dmmt_parse_ppm, dmmt_read_ppm, dmmt_parse_ppm_header, dmmt_decode_ppm_device,
  * dmmt_convert_ppm_to_jpeg) returned on the calling thread: IncompletePixelParsed(n) -> n

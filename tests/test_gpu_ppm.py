@@ -289,6 +289,74 @@ def test_convert_device_batch(encoder, spec_tables):
             encoder.free(p)
 
 
+def _device_files(encoder, datas, allocs):
+    L = dmmt_jpeg.lib()
+    files = []
+    for data in datas:
+        hdr = dmmt_jpeg.parse_ppm_header(data)
+        cap = L.dmmt_max_jpeg_bytes(max(hdr.width, 1), max(hdr.height, 1), 2)
+        d_text, d_out, d_len = encoder.malloc(len(data)), encoder.malloc(cap), encoder.malloc(4)
+        allocs += [d_text, d_out, d_len]
+        encoder.h2d(d_text, np.frombuffer(data, np.uint8))
+        files.append((d_text, len(data), hdr, d_out, cap, d_len))
+    return files
+
+
+def test_convert_device_batch_error_payload_is_the_first_failures(encoder):
+    """dmmt_convert_ppm_device_batch returns the first failing file's code, and the
+    payload dmmt_last_error_detail keeps is that file's (IncompletePixelParsed(1)),
+    not the one of a file redone after it (a commented file that succeeds, then
+    IncompletePixelParsed(2)) [ppm.rs:239-245, error.rs:3-22]"""
+    rng = np.random.default_rng(5)
+    rgb = rng.integers(0, 256, (12, 20, 3), dtype=np.uint8)
+    body = b" ".join(b"%d" % v for v in rgb.reshape(-1))
+    datas = [b"P3 2 2 255\n" + b"9 " * 10 + b" " * 100,              # 10 samples: n = 1
+             b"P3 20 12 255\n# a comment\n" + body + b"\n",          # redone, succeeds
+             b"P3 2 2 255\n" + b"9 " * 11 + b" " * 100]              # 11 samples: n = 2
+    allocs = []
+    try:
+        files = _device_files(encoder, datas, allocs)
+        for lanes in (1, 3):
+            encoder.set_lanes(lanes)
+            with pytest.raises(dmmt_jpeg.Error) as e:
+                encoder.convert_ppm_device_batch(files, dmmt_jpeg.JpegTransformationOptions())
+            assert e.value.code == -3 and e.value.n == 1, str(e.value)
+            assert "got 1." in str(e.value)
+            codes = encoder.convert_ppm_device_batch(files, dmmt_jpeg.JpegTransformationOptions(), check=False)
+            assert codes == [-3, 0, -3]
+            assert dmmt_jpeg.lib().dmmt_last_error_detail() == 1
+    finally:
+        encoder.set_lanes(1)
+        for p in allocs:
+            encoder.free(p)
+
+
+def test_convert_device_batch_redoes_only_the_failing_file(encoder, spec_tables):
+    """A commented file in a batch is redone on its own; the clean files on its lane
+    are not (each speculative encode reports into its own status words), and every
+    JPEG is the oracle's"""
+    rng = np.random.default_rng(6)
+    cases = []
+    for k in range(12):
+        rgb = rng.integers(0, 256, (24 + k, 40, 3), dtype=np.uint8)
+        cases.append((p3_text(rgb, 255, rng, comments=0.05 if k == 4 else 0.0), rgb))
+    allocs = []
+    try:
+        files = _device_files(encoder, [d for d, _ in cases], allocs)
+        for lanes in (1, 2):
+            encoder.set_lanes(lanes)
+            codes = encoder.convert_ppm_device_batch(files, dmmt_jpeg.JpegTransformationOptions())
+            assert codes == [0] * len(cases)
+            assert encoder.batch_redone() == 1
+            for (d_text, n, hdr, d_out, cap, d_len), (data, rgb) in zip(files, cases):
+                size = int(np.frombuffer(encoder.d2h(d_len, 4), np.uint32)[0])
+                assert encoder.d2h(d_out, size) == oracle.encode(rgb, 255, 2, *spec_tables)
+    finally:
+        encoder.set_lanes(1)
+        for p in allocs:
+            encoder.free(p)
+
+
 def _random_file(rng):
     """a random small PPM file: P3 (separators, sometimes comments, signs, leading
     zeros, a broken token, a missing or extra sample, a sample above maxval) or P6"""
