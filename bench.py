@@ -121,11 +121,8 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
         n, off, total = step()
     barrier_sync(enc)
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=torch.device("cuda", local_rank) if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # (strong scaling: each rank's rate is its stripe's pixels over its own time)
+    elapsed, ranks = gather_ranks(elapsed, world, enc, w * (y1 - y0) * args.steps)
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:  # the oracle on a bounded stripe of the same image (256 pixel rows)
@@ -158,6 +155,7 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
                 "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
                 "restart_interval": mcux * rpi, "parallelism": f"MCU-row stripes x{world}",
                 "jpeg_bytes": int(total) if total is not None else int(n),
+                "ranks": ranks,
             },
             "roofline": None,
             "cpu_baseline": cpu,
@@ -169,6 +167,27 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
     enc.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def gather_ranks(elapsed, world, enc, pixels_per_rank):
+    """every rank's own timed region and GPU, gathered on every rank, so that the
+    line validates itself: the reported elapsed is their MAX, each rank's own rate
+    is listed, and each rank names the device its context runs on (checked by
+    dmmt_ctx_check_device: the thread's device and every pooled buffer on it)"""
+    device = int(enc.check_device())
+    secs, devs, backend = [elapsed], [device], None
+    if world > 1:
+        backend = dist.get_backend()
+        t = torch.tensor([elapsed, float(device)], dtype=torch.float64,
+                         device=torch.device("cuda", device) if backend == "nccl" else "cpu")
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        secs = [float(x[0].item()) for x in out]
+        devs = [int(x[1].item()) for x in out]
+    info = {"world_size": world, "backend": backend, "seconds": [round(x, 6) for x in secs],
+            "mpixel_s": [round(pixels_per_rank / x / 1e6, 2) for x in secs], "devices": devs,
+            "one_device_per_rank": len(set(devs)) == world}
+    return max(secs), info
 
 
 def run_inproc(args, emit, make_group):
@@ -641,10 +660,7 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
     if args.mall_compare:  # inputs resident in the Infinity Cache: 4 slots
         extra["mall_resident_4_slots"] = timed(lanes, min(4, nslots))
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, ranks = gather_ranks(elapsed, world, enc, w * h * fps * args.steps)
 
     lens = np.frombuffer(enc.d2h(d_len[0], 4 * fps), np.uint32)
     jpeg_bytes = float(lens.mean())
@@ -683,7 +699,7 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
                         f"over {nslots} distinct slots ({nslots * slot_bytes / 2**20:.0f} MiB: streamed from HBM)",
             "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
             "frames_per_step": fps, "mean_jpeg_bytes": jpeg_bytes, "parallelism": f"independent frames x{world}",
-            "lanes": lanes, "input_slots": nslots,
+            "lanes": lanes, "input_slots": nslots, "ranks": ranks,
         }
         if "mall_resident_4_slots" in extra:
             t4 = extra["mall_resident_4_slots"]

@@ -188,4 +188,70 @@ __device__ __forceinline__ void raise_status(int* status, int bits) {
     }
 }
 
+// "Last arriver does the rest" (k_hist's Huffman tables, k_emit's chunk
+// offsets): a kernel's workgroups count themselves in per frame on two levels of
+// counters, each on its own 128-byte line -- workgroup i into group i mod
+// kArriveGroups, the last of a group into the frame's top counter (atomics on one
+// address serialise: 1519 on a single counter cost ~18 us) -- and the one that
+// sees itself last does the frame's remaining work; no workgroup ever waits.
+// Every counter is reset by its last arriver, so they are zero between launches
+// (any kernel of the stream may use them next).
+// Ordering.  The shipped form (DMMT_ARRIVE_FORMAL=0) rests on gfx950's memory
+// system, not on the HIP memory model's release/acquire:
+//   what                                   emitted (gfx950)            why it is ordered
+//   results: agent-scope atomic stores     global_store ... sc1        sc1: written through past the
+//     (k_emit) / device atomics (k_hist)   global_atomic_add           XCD's L2; atomics execute at the
+//                                                                      memory side of the L2s
+//   every result-writing wave              s_waitcnt vmcnt(0)          gfx9 counts stores and atomics in
+//                                                                      vmcnt: they have completed
+//   barrier, then thread 0's increments    s_barrier; global_atomic    issued after the completions
+//   last arriver's reads                   global_load ... sc1         sc1: not served from a stale L1
+// so the last arriver reads every result.  The formal form (DMMT_ARRIVE_FORMAL=1:
+// a RELEASE increment of the group counter, ACQ_REL of the top counter, an
+// agent-scope ACQUIRE fence in the last workgroup -- happens-before under the HIP
+// model) makes the compiler emit buffer_wbl2 sc1 (a write-back of the XCD's L2)
+// before every workgroup's increment: measured on MI355X (round 5, 4K q90, one
+// lane) k_emit 31.4 -> 50.8 us and the 4-lane bench 151 -> 68 Gpixel/s
+// (profiles/r05_v01_*), so it stays a build option for studies.  The inline
+// s_waitcnt is an asm statement with a memory clobber: the compiler can move no
+// memory access across it, and the relaxed atomics around it keep their order.
+#ifndef DMMT_ARRIVE_FORMAL
+#define DMMT_ARRIVE_FORMAL 0
+#endif
+constexpr int kArriveGroups = 64, kArriveStride = 32;              // counters 128 bytes apart
+constexpr int kArriveWords = (kArriveGroups + 1) * kArriveStride;  // per frame (kernels.hpp: kArriveFrameWords)
+
+// one thread per workgroup: true in the frame's last workgroup (idx of count)
+__device__ __forceinline__ bool arrive_last(uint32_t* fa, unsigned idx, unsigned count) {
+#if DMMT_ARRIVE_FORMAL
+    constexpr int kOrder = __ATOMIC_RELEASE, kTopOrder = __ATOMIC_ACQ_REL;
+#else
+    constexpr int kOrder = __ATOMIC_RELAXED, kTopOrder = __ATOMIC_RELAXED;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the results' stores / atomics have completed
+#endif
+    const unsigned grp = idx % kArriveGroups;
+    const unsigned ngrp = count < (unsigned)kArriveGroups ? count : (unsigned)kArriveGroups;
+    const uint32_t in_grp = (count - grp + kArriveGroups - 1) / kArriveGroups;
+    bool last = false;
+    if (__hip_atomic_fetch_add(fa + grp * kArriveStride, 1u, kOrder, __HIP_MEMORY_SCOPE_AGENT) == in_grp - 1u) {
+        __hip_atomic_store(fa + grp * kArriveStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t* const top = fa + kArriveGroups * kArriveStride;
+        last = __hip_atomic_fetch_add(top, 1u, kTopOrder, __HIP_MEMORY_SCOPE_AGENT) == ngrp - 1u;
+        if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return last;
+}
+
+// every thread of the frame's last workgroup, after the barrier that told it so
+__device__ __forceinline__ void arrive_acquire() {
+#if DMMT_ARRIVE_FORMAL
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
+
+// a load of another workgroup's result (agent scope)
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace dmmt

@@ -40,6 +40,10 @@ struct EventPair {
 // One instantiated capture of the whole per-call pipeline.  The key holds every
 // value baked into the launches (pointers, geometry, stream), so a hit replays
 // exactly the launches a direct enqueue would make.
+#ifndef DMMT_FUSE_TABLES_DEFAULT
+#define DMMT_FUSE_TABLES_DEFAULT 1  // (measurement builds: 0)
+#endif
+
 struct GraphEntry {
     std::vector<uint64_t> key;
     hipGraphExec_t exec = nullptr;
@@ -110,6 +114,9 @@ struct dmmt_ctx {
     int stage_launches[ST_COUNT] = {0};
     // replayed pipelines (opt-in: DMMT_GRAPHS=1; measured no faster than direct launches on 4K frames)
     bool use_graphs = false;
+    // k_tables fused into k_hist's last workgroup where tables_fusable (DMMT_FUSE_TABLES=0: the
+    // separate launch, for measurements)
+    bool fuse_tables = DMMT_FUSE_TABLES_DEFAULT != 0;
     std::vector<GraphEntry> graphs;
     uint64_t graph_clock = 0;
     // MCU-row stripe between dmmt_stripe_analyze and dmmt_stripe_encode
@@ -345,11 +352,14 @@ struct StageTimer {
 // occur (Image<f32> input, host blocks).
 int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bits, uint8_t* out, size_t out_stride,
                       uint32_t* out_len, hipStream_t st, int check_cat, bool hist_done = false) {
-    if (!hist_done) {  // (a stripe's differences and counts come from dmmt_stripe_analyze)
+    // (a stripe's differences and counts come from dmmt_stripe_analyze; else, when
+    // tables_fusable, k_hist's last workgroup per frame builds the tables)
+    const bool fused_tables = !hist_done && c->fuse_tables && tables_fusable(g);
+    if (!hist_done) {
         StageTimer t(c, ST_HIST, st);
-        HIP_TRY(launch_hist(nf, g, w, check_cat, st));
+        HIP_TRY(launch_hist(nf, g, w, check_cat, st, fused_tables, bits, out, out_stride));
     }
-    {
+    if (!fused_tables) {
         StageTimer t(c, ST_TABLES, st);
         HIP_TRY(launch_tables(nf, g, w, bits, out, out_stride, st));
     }
@@ -516,6 +526,7 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
     dmmt_ctx* c = new dmmt_ctx();
     c->device = device;
     if (const char* e = getenv("DMMT_GRAPHS")) c->use_graphs = atoi(e) != 0;
+    if (const char* e = getenv("DMMT_FUSE_TABLES")) c->fuse_tables = atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return DMMT_E_HIP;
@@ -529,6 +540,50 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
     }
     *out = c;
     return DMMT_OK;
+}
+
+// The context's device is the calling thread's current one after set_device, and
+// every pooled device buffer it holds (lane workspaces, tables, staging) was
+// allocated on that device -- the multi-GPU readiness check a group's worker runs
+// before a member's work (a member's buffers landing on another GPU would still
+// compute correctly over the xGMI mapping, slowly and silently).
+static int check_ptr_device(const void* p, int dev) {
+    if (!p) return DMMT_OK;
+    hipPointerAttribute_t a;
+    HIP_TRY(hipPointerGetAttributes(&a, p));
+    return a.device == dev ? DMMT_OK : DMMT_E_DEVICE_MISMATCH;
+}
+
+namespace dmmt {
+int ctx_check_device(dmmt_ctx* c) {
+    int rc;
+    if ((rc = set_device(c))) return rc;
+    int cur = -1;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur != c->device) return DMMT_E_DEVICE_MISMATCH;
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (Lane* L : c->lanes) {
+        const DevBuf* bufs[] = {&L->coef,       &L->dcdiff,   &L->lastnz,     &L->ac_hist,    &L->dc_hist,
+                                &L->code_tab,   &L->hdr_len,  &L->total_out,  &L->stage,      &L->chunk_bits,
+                                &L->chunk_ff,   &L->chunk_edge, &L->chunk_bit0, &L->chunk_out, &L->arrive,
+                                &L->ppm_rgb,    &L->ppm_counts, &L->ppm_rowbase};
+        for (const DevBuf* b : bufs)
+            if ((rc = check_ptr_device(b->p, c->device))) return rc;
+    }
+    const DevBuf* bufs[] = {&c->lut, &c->qtab, &c->qtab_u8, &c->in, &c->out, &c->out_len, &c->dct, &c->ppm_text,
+                            &c->ppm_maps, &c->ppm_chunk_in, &c->ppm_misc, &c->ppm_counts};
+    for (const DevBuf* b : bufs)
+        if ((rc = check_ptr_device(b->p, c->device))) return rc;
+    return DMMT_OK;
+}
+int ptr_check_device(const void* p, int device) { return check_ptr_device(p, device); }
+}  // namespace dmmt
+
+extern "C" int dmmt_ctx_check_device(dmmt_ctx* c, int32_t* device) {
+    if (!c) return DMMT_E_INVALID_ARGUMENT;
+    if (device) *device = c->device;
+    if (c->group) return dmmt::group_check_devices(c->group);
+    return dmmt::ctx_check_device(c);
 }
 
 extern "C" int dmmt_ctx_create_multi(const int* device_ids, int n, dmmt_ctx** out) {
@@ -1200,6 +1255,7 @@ extern "C" const char* dmmt_error_name(int code) {
     case DMMT_E_OUT_OF_MEMORY: return "OutOfMemory";
     case DMMT_E_NO_DEVICE: return "NoDevice";
     case DMMT_E_CAPACITY: return "Capacity";
+    case DMMT_E_DEVICE_MISMATCH: return "DeviceMismatch";
     default: return "Unknown";
     }
 }
@@ -1225,6 +1281,7 @@ extern "C" const char* dmmt_strerror(int code) {
     case DMMT_E_OUT_OF_MEMORY: return "Out of device memory";
     case DMMT_E_NO_DEVICE: return "No gfx950 (MI355X) device available; this library has no CPU fallback";
     case DMMT_E_CAPACITY: return "Output buffer too small";
+    case DMMT_E_DEVICE_MISMATCH: return "A member context's thread or buffer is not on its GPU";
     default: return dmmt_error_name(code);
     }
 }

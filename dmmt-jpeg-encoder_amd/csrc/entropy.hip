@@ -54,19 +54,6 @@ constexpr int kEmitOcc = kChunkBlocks == 256 ? 7 : 3;  // workgroups per CU
 constexpr int kEmitWords = 4 * kChunkBlocks;
 // Bytes per pass of k_stuffwrite (16 per thread).
 constexpr int kStuffPass = 4096;
-// The fused offsets' hand-off (k_emit): 1 = release / acquire ordering under the
-// HIP memory model; 0 = the round-4 form (relaxed atomics after an s_waitcnt
-// vmcnt(0), correct by the gfx950 ISA argument of DESIGN.md 3; measurement builds)
-#ifndef DMMT_ARRIVE_FORMAL
-#define DMMT_ARRIVE_FORMAL 1
-#endif
-#if DMMT_ARRIVE_FORMAL
-#define DMMT_ARRIVE_ORDER __ATOMIC_RELEASE
-#define DMMT_ARRIVE_TOP_ORDER __ATOMIC_ACQ_REL
-#else
-#define DMMT_ARRIVE_ORDER __ATOMIC_RELAXED
-#define DMMT_ARRIVE_TOP_ORDER __ATOMIC_RELAXED
-#endif
 #ifndef DMMT_EMIT_PRIO
 #define DMMT_EMIT_PRIO 1  // k_emit's wave priorities by walk length (0: off, study builds)
 #endif
@@ -274,8 +261,6 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
                               const uint32_t* __restrict__ cedge, const Geom& g, unsigned long long* __restrict__ bit0,
                               unsigned long long* __restrict__ outo, unsigned long long* __restrict__ total,
                               unsigned long long* sWaveV, int* sWaveF);
-constexpr int kArriveGroups = 64, kArriveStride = 32;                 // counters 128 bytes apart
-constexpr int kArriveWords = (kArriveGroups + 1) * kArriveStride;  // per frame (kernels.hpp: kArriveFrameWords)
 static_assert(kArriveWords == kArriveFrameWords, "the host sizes the counters");
 
 // ---------------------------------------------------------------------- k_emit
@@ -503,42 +488,11 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         __hip_atomic_store(chunk_bits + cid, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(chunk_edge + cid, (first16 << 16) | last16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (fuse) {  // (uniform) count this workgroup in once its summary has reached memory
-        // Two levels of counters, each on its own 128-byte line: chunk c counts into
-        // group c mod kArriveGroups, the last of a group into the frame's top
-        // counter (atomics on one address serialise: 1519 on a single counter cost
-        // ~18 us); every counter is reset by its last arriver.
-        // Ordering (HIP / C++ memory model, agent scope): thread 0 stored the
-        // summary and publishes it with a RELEASE increment of its group counter;
-        // the group's last arriver increments the top counter ACQ_REL (it acquires
-        // the group's releases and releases them on, a release sequence); the
-        // frame's last arriver thus happens-after every summary store, and its
-        // threads take an agent-scope ACQUIRE fence after the barrier that hands
-        // them the verdict before their agent-scope loads of the summaries.
-        if (tid == 0) {
-            uint32_t* const fa = arrive + (size_t)frame * kArriveWords;
-            const int grp = (int)(chunk % kArriveGroups);
-            const int ngrp = min(g.nch, kArriveGroups);
-            const uint32_t in_grp = (uint32_t)((g.nch - grp + kArriveGroups - 1) / kArriveGroups);
-            bool last = false;
-#if !DMMT_ARRIVE_FORMAL
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the summary stores have completed (sc1: past L2)
-#endif
-            if (__hip_atomic_fetch_add(fa + grp * kArriveStride, 1u, DMMT_ARRIVE_ORDER, __HIP_MEMORY_SCOPE_AGENT) ==
-                in_grp - 1u) {
-                __hip_atomic_store(fa + grp * kArriveStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint32_t* const top = fa + kArriveGroups * kArriveStride;
-                last = __hip_atomic_fetch_add(top, 1u, DMMT_ARRIVE_TOP_ORDER, __HIP_MEMORY_SCOPE_AGENT) ==
-                       (uint32_t)ngrp - 1u;
-                if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            sLast = last;
-        }
+    if (fuse) {  // (uniform) count this workgroup in once its summary is published (arrive_last)
+        if (tid == 0) sLast = arrive_last(arrive + (size_t)frame * kArriveWords, chunk, (unsigned)g.nch);
         __syncthreads();
         if (sLast) {  // every other chunk of the frame is done: its offsets
-#if DMMT_ARRIVE_FORMAL
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
+            arrive_acquire();
             const size_t fb = (size_t)frame * g.nch;
             fused_offsets(chunk_bits + fb, chunk_ff + fb * 8, chunk_edge + fb, g, chunk_bit0 + fb, chunk_out + fb,
                           total_out + frame, sOffV, sOffF);
@@ -677,9 +631,6 @@ __device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigne
 static_assert(kFusedRoundChunks % kEmitThreads == 0, "whole chunks per thread of the fused offsets");
 static_assert((unsigned long long)kFusedOffsetsMaxChunks * kChunkBlocks * kMaxBlockBits < (1ull << 32),
               "a fused frame's bit offsets fit 32 bits");
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ cff,
                               const uint32_t* __restrict__ cedge, const Geom& g, unsigned long long* __restrict__ bit0,
                               unsigned long long* __restrict__ outo, unsigned long long* __restrict__ total,

@@ -39,6 +39,11 @@ int stripes_on_contexts(dmmt_ctx* const* ctxs, void* workers, int n, const dmmt_
 // device-resident frames, frames[i] on member i, enqueued without waiting
 int group_encode_device(Group* g, const dmmt_device_frames* frames, int n, const dmmt_options* opt);
 int group_synchronize(Group* g);
+// every member checked on its worker thread (ctx_check_device + the group's staging buffers)
+int group_check_devices(Group* g);
+// encoder.cpp: the calling thread's device and every pooled buffer of c on c's GPU
+int ctx_check_device(dmmt_ctx* c);
+int ptr_check_device(const void* p, int device);
 int group_set_lanes(Group* g, int n);
 int group_set_profiling(Group* g, int enable);
 int group_profile(Group* g, double* ms, int32_t* launches, int n_stages);

@@ -31,6 +31,7 @@
 #include "device_common.hpp"
 #include "jpeg_common.hpp"
 #include "kernels.hpp"
+#include "wave_merge.hpp"
 
 namespace dmmt {
 
@@ -574,16 +575,37 @@ struct HistCoef {
     uint32_t w[32];  // zigzag position 2i in the low half of w[i], 2i+1 in the high half
 };
 
-template <bool CHECK>
-__global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, int16_t* __restrict__ dcdiff,
+// (the fused tables, defined below)
+constexpr int kTailSmallWords = 4 + 4 * 16;
+__device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_hist, const uint32_t* dc_hist, int frame,
+                                            const Geom& g, uint32_t* __restrict__ code_tab, uint8_t* __restrict__ out,
+                                            size_t out_stride, uint32_t* __restrict__ hdr_len,
+                                            const uint8_t* __restrict__ qtab_u8, int bits_per_channel,
+                                            int* __restrict__ status, int* sCnt, int* sBits);
+constexpr int kHistCopies = 4, kHistCopyWords = 545;
+constexpr int kTailLdsBytes = 7072;  // tables_tail's per-table regions (static_assert below)
+
+// FUSE (tables_fusable): the frame's last workgroup to finish also builds the four
+// Huffman tables and the header (tables_tail), so no k_tables launch follows.
+// Eight waves per SIMD (at most 64 VGPRs): the tail alone would take more, and the
+// histogram loop wants the occupancy.
+template <bool CHECK, bool FUSE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_hist(const int16_t* __restrict__ coef, int16_t* __restrict__ dcdiff,
                                               uint8_t* __restrict__ lastnz, Geom g,
                                               uint32_t* __restrict__ ac_hist /*[frames][reps][2][256]*/,
                                               uint32_t* __restrict__ dc_hist /*[frames][reps][2][16]*/,
-                                              int* __restrict__ status) {
+                                              int* __restrict__ status, uint32_t* __restrict__ arrive,
+                                              uint32_t* __restrict__ code_tab, uint8_t* __restrict__ out,
+                                              size_t out_stride, uint32_t* __restrict__ hdr_len,
+                                              const uint8_t* __restrict__ qtab_u8, int bits_per_channel) {
     // four copies of the histograms (lane & 3): the lanes of a wave often count
-    // the same symbol at the same position; 545 words apart (different banks)
-    constexpr int NC = 4, HS = 545;
-    __shared__ uint32_t sH[NC * HS];  // per copy: [AC luma 256][AC chroma 256][DC luma 16][DC chroma 16]
+    // the same symbol at the same position; 545 words apart (different banks).
+    // FUSE: the same LDS then holds the tables' work (tables_tail).
+    constexpr int NC = kHistCopies, HS = kHistCopyWords;
+    constexpr int kWords = FUSE && kTailLdsBytes / 4 > NC * HS ? kTailLdsBytes / 4 : NC * HS;
+    __shared__ __attribute__((aligned(16))) uint32_t sH[kWords];  // per copy: [AC luma 256][AC chroma 256][DC luma 16][DC chroma 16]
+    __shared__ int sSmall[FUSE ? kTailSmallWords : 1];
+    __shared__ uint32_t sLastWg;
     const int tid = threadIdx.x;
     const int frame = blockIdx.y;
     for (int i = tid; i < NC * HS; i += 256) sH[i] = 0;
@@ -673,6 +695,19 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
         else
             atomicAdd(&dc_hist[rep * 32 + (i - 512)], v);
     }
+    if (FUSE) {  // count this workgroup in (arrive_last); the frame's last one builds the tables
+#if !DMMT_ARRIVE_FORMAL
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's flush atomics have completed
+#endif
+        __syncthreads();  // (also: every wave's sH reads are done before the tail reuses the LDS)
+        if (tid == 0) sLastWg = arrive_last(arrive + (size_t)frame * kArriveWords, blockIdx.x, gridDim.x);
+        __syncthreads();
+        if (sLastWg) {
+            arrive_acquire();
+            tables_tail(reinterpret_cast<uint8_t*>(sH), ac_hist, dc_hist, frame, g, code_tab, out, out_stride, hdr_len,
+                        qtab_u8, bits_per_channel, status, sSmall, sSmall + 4);
+        }
+    }
 }
 
 // ============================================================== k_tables
@@ -702,6 +737,83 @@ __global__ __launch_bounds__(256) void k_hist(const int16_t* __restrict__ coef, 
 __device__ __forceinline__ void put_be16(uint8_t* p, int v) {
     p[0] = (uint8_t)(v >> 8);
     p[1] = (uint8_t)v;
+}
+
+// The table's DHT segment (encoder.rs:169-181: BITS, then the symbols most frequent
+// first, i.e. symrank -- symbols by ascending frequency -- reversed) and, for table
+// 0, SOI, APP0, DQT x2, SOF0, [DRI], SOS (encoder.rs:125-262) and the header length;
+// a later stripe of an image (dmmt_stripe_*) writes no header.  Written by threads
+// t0, t0 + step, ... of the table (k_tables: 256 per table; k_hist's fused tail: 64).
+__device__ void write_table_header(uint8_t* o, int tab, int t0, int step, int n, const int nt[4],
+                                   const uint8_t* symrank, const int* bits16, const Geom& g,
+                                   const uint8_t* __restrict__ qtab_u8, int bits_per_channel, uint32_t* hdr_len) {
+    if (!g.stripe_first) {  // a later stripe of an image: tables only, no header
+        if (tab == 0 && t0 == 0) *hdr_len = 0;
+        return;
+    }
+    const int pos_dht0 = 2 + 18 + 69 + 69 + 19;
+    const int off_lac = pos_dht0;
+    const int off_ldc = off_lac + 21 + nt[1];
+    const int off_cac = off_ldc + 21 + nt[0];
+    const int off_cdc = off_cac + 21 + nt[3];
+    const int dht = tab == 0 ? off_ldc : tab == 1 ? off_lac : tab == 2 ? off_cdc : off_cac;
+    for (int s = t0; s < n; s += step) o[dht + 21 + s] = symrank[n - 1 - s];  // DHT symbols in reversed order (encoder.rs:180)
+    for (int s = t0; s < 16; s += step) o[dht + 5 + s] = (uint8_t)bits16[s];
+    if (t0 == 0) {
+        uint8_t* d = o + dht;
+        d[0] = 0xFF;
+        d[1] = 0xC4;
+        put_be16(d + 2, 2 + 17 + n);
+        const uint8_t kind[4] = {0x00, 0x11, 0x02, 0x13};  // encoder.rs:92-98 TableKind
+        d[4] = kind[tab];
+    }
+    if (tab != 0) return;
+    const int pos_after_dht = pos_dht0 + 4 * 21 + nt[0] + nt[1] + nt[2] + nt[3];
+    const int pos_sos = pos_after_dht + (g.restart_interval > 0 ? 6 : 0);
+    if (t0 == 0) {
+        o[0] = 0xFF;
+        o[1] = 0xD8;  // SOI
+        const uint8_t app0[18] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0, 0x01, 0x02, 0x00, 0x00, 0x48, 0x00, 0x48, 0, 0};
+        for (int i = 0; i < 18; ++i) o[2 + i] = app0[i];
+        for (int q = 0; q < 2; ++q) {  // DQT, table in zigzag order (encoder.rs:193-212)
+            uint8_t* d = o + 20 + 69 * q;
+            d[0] = 0xFF;
+            d[1] = 0xDB;
+            put_be16(d + 2, 67);
+            d[4] = (uint8_t)q;
+        }
+        uint8_t* sof = o + 158;  // encoder.rs:227-245
+        sof[0] = 0xFF;
+        sof[1] = 0xC0;
+        put_be16(sof + 2, 17);
+        sof[4] = (uint8_t)bits_per_channel;
+        put_be16(sof + 5, g.sof_height);
+        put_be16(sof + 7, g.width);
+        sof[9] = 3;
+        sof[10] = 1;
+        sof[11] = (uint8_t)((g.hr << 4) | g.vr);
+        sof[12] = 0;
+        sof[13] = 2;
+        sof[14] = 0x11;
+        sof[15] = 1;
+        sof[16] = 3;
+        sof[17] = 0x11;
+        sof[18] = 1;
+        if (g.restart_interval > 0) {  // extension: DRI
+            uint8_t* d = o + pos_after_dht;
+            d[0] = 0xFF;
+            d[1] = 0xDD;
+            put_be16(d + 2, 4);
+            put_be16(d + 4, g.restart_interval);
+        }
+        const uint8_t sos[14] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x01, 0x02, 0x23, 0x03, 0x23, 0x00, 0x3F, 0x00};
+        for (int i = 0; i < 14; ++i) o[pos_sos + i] = sos[i];
+        *hdr_len = (uint32_t)(pos_sos + 14);
+    }
+    for (int s = t0; s < 128; s += step) {
+        const int q = s >> 6, i = s & 63;
+        o[20 + 69 * q + 5 + i] = qtab_u8[q * 64 + c_zigzag[i]];
+    }
 }
 
 // #{j < m : pair sum prev[2j] + prev[2j+1] < x}, known to be >= lb (sums ascending)
@@ -925,77 +1037,327 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
 
     // ---- 6: header
     if (!sym_thread) return;
-    if (!g.stripe_first) {  // a later stripe of an image: tables only, no header
-        if (tab == 0 && s == 0) hdr_len[frame] = 0;
-        return;
-    }
-    uint8_t* o = out + (size_t)frame * out_stride;
-    const int pos_dht0 = 2 + 18 + 69 + 69 + 19;
-    const int off_lac = pos_dht0;
-    const int off_ldc = off_lac + 21 + nt[1];
-    const int off_cac = off_ldc + 21 + nt[0];
-    const int off_cdc = off_cac + 21 + nt[3];
-    const int dht = tab == 0 ? off_ldc : tab == 1 ? off_lac : tab == 2 ? off_cdc : off_cac;
-    if (s < n) o[dht + 21 + s] = sSym[n - 1 - s];  // DHT symbols in reversed order (encoder.rs:180)
-    if (s < 16) o[dht + 5 + s] = (uint8_t)sBits[s];
-    if (s == 0) {
-        uint8_t* d = o + dht;
-        d[0] = 0xFF;
-        d[1] = 0xC4;
-        put_be16(d + 2, 2 + 17 + n);
-        const uint8_t kind[4] = {0x00, 0x11, 0x02, 0x13};  // encoder.rs:92-98 TableKind
-        d[4] = kind[tab];
-    }
-    if (tab == 0) {
-        const int pos_after_dht = pos_dht0 + 4 * 21 + nt[0] + nt[1] + nt[2] + nt[3];
-        const int pos_sos = pos_after_dht + (g.restart_interval > 0 ? 6 : 0);
-        if (s == 0) {
-            o[0] = 0xFF;
-            o[1] = 0xD8;  // SOI
-            const uint8_t app0[18] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0, 0x01, 0x02, 0x00, 0x00, 0x48, 0x00, 0x48, 0, 0};
-            for (int i = 0; i < 18; ++i) o[2 + i] = app0[i];
-            for (int q = 0; q < 2; ++q) {  // DQT, table in zigzag order (encoder.rs:193-212)
-                uint8_t* d = o + 20 + 69 * q;
-                d[0] = 0xFF;
-                d[1] = 0xDB;
-                put_be16(d + 2, 67);
-                d[4] = (uint8_t)q;
-            }
-            uint8_t* sof = o + 158;  // encoder.rs:227-245
-            sof[0] = 0xFF;
-            sof[1] = 0xC0;
-            put_be16(sof + 2, 17);
-            sof[4] = (uint8_t)bits_per_channel;
-            put_be16(sof + 5, g.sof_height);
-            put_be16(sof + 7, g.width);
-            sof[9] = 3;
-            sof[10] = 1;
-            sof[11] = (uint8_t)((g.hr << 4) | g.vr);
-            sof[12] = 0;
-            sof[13] = 2;
-            sof[14] = 0x11;
-            sof[15] = 1;
-            sof[16] = 3;
-            sof[17] = 0x11;
-            sof[18] = 1;
-            if (g.restart_interval > 0) {  // extension: DRI
-                uint8_t* d = o + pos_after_dht;
-                d[0] = 0xFF;
-                d[1] = 0xDD;
-                put_be16(d + 2, 4);
-                put_be16(d + 4, g.restart_interval);
-            }
-            const uint8_t sos[14] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x01, 0x02, 0x23, 0x03, 0x23, 0x00, 0x3F, 0x00};
-            for (int i = 0; i < 14; ++i) o[pos_sos + i] = sos[i];
-            hdr_len[frame] = (uint32_t)(pos_sos + 14);
-        }
-        if (s < 128) {
-            const int q = s >> 6, i = s & 63;
-            o[20 + 69 * q + 5 + i] = qtab_u8[q * 64 + c_zigzag[i]];
-        }
-    }
+    write_table_header(out + (size_t)frame * out_stride, tab, s, 256, n, nt, sSym, sBits, g, qtab_u8, bits_per_channel,
+                       hdr_len + frame);
     DMMT_TRACE(15);
     DMMT_TRACE_FLUSH(0, 1);
+}
+
+// ============================================================== fused tables
+// k_tables' work done by k_hist's last workgroup of a frame (tables_fusable): wave
+// t builds table t (0 luma DC, 1 luma AC, 2 chroma DC, 3 chroma AC).  Frequencies in
+// 32 bits: the host fuses only frames whose symbol counts, and thus every package
+// weight (at most 15 times their sum), stay below 2^30.  The phases of k_tables:
+//  1 the 8 replicas summed (agent-scope loads after the arrival); symbol s = lane
+//    + 64 q; present symbols compacted as keys (frequency << 8 | s), u32 when
+//    every frequency is below 2^24, else u64
+//  2 rank = present keys below mine (symbol_counting.rs:92-94's stable ascending
+//    sort over the f > 0 filter of 25-32)
+//  3 package-merge, limit 15 (length_limited.rs:37-134), in registers: level k is
+//    the merge of the leaves (ascending) with the pair sums of level k-1
+//    (ascending), ties leaf first -- keys (weight << 1 | is_package), one
+//    bitonic merger of the wave (wave_merge.hpp) per level, the package
+//    positions of every level kept as 64-bit masks (a ballot per register slot,
+//    parked in a lane of a VGPR)
+//  4 the solution from the deepest level (n-1 packages), every lane alike, lengths,
+//    +1 on the least frequent (symbol_counting.rs:85-90)
+//  5 canonical codes over the reversed list (huffman/encoder.rs:45-67,116-119)
+//  6 the DHT segment, and for table 0 the rest of the header (write_table_header)
+// One barrier: before 6 (every table's symbol count).  LDS per table (bytes):
+// F u32[cap] | the keys u64[cap] | Sym u8[cap]; cap = 256 for the AC tables, 16 DC.
+#ifndef DMMT_TAIL_STOP
+#define DMMT_TAIL_STOP 0
+#endif
+constexpr int kTailLevels = 15;
+constexpr int kTailBase[4] = {0, 208, 3536, 3744};
+static_assert(kTailBase[3] + 3328 == kTailLdsBytes, "tables_tail's LDS regions");
+
+// The tail's phases pass data between the lanes of ONE wave through LDS: a wave's
+// LDS operations complete in order, so no s_barrier -- only no code motion across.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Levels 1-14 of the package-merge over n leaves F (ascending) in 64 * EPL element
+// merges (n <= 32 * EPL): slot-major, the leaves ascending in the lower half
+// (static), the packages DESCENDING in the upper (element S/2 + m holds package
+// S/2 - 1 - m), so each level is one bitonic merge.  Level k's package positions
+// (a ballot per slot) and the packages before each slot are kept in lane k EPL + s
+// of two VGPR pairs, and the solution chain reads them back
+// (readlane): leaf[k] = the leaves in the solution prefix of level k.
+template <int EPL>
+__device__ __forceinline__ void tail_levels(const uint32_t* F, int n, int (&leaf)[kTailLevels]) {
+    const int lane = lane_id();
+    constexpr int H = EPL == 1 ? 1 : EPL / 2;  // register slots per half (EPL 1: lanes 0-31 / 32-63)
+    // leaf index of lower-half slot t / package index of upper-half slot t in this lane
+    auto leaf_index = [&](int t) { return EPL == 1 ? lane : 64 * t + lane; };
+    auto pkg_index = [&](int t) { return EPL == 1 ? 63 - lane : 32 * EPL - 1 - 64 * t - lane; };
+    uint32_t lk[H], pk[H];
+    int np = n >> 1;
+#pragma unroll
+    for (int t = 0; t < H; ++t) {
+        const int i = leaf_index(t), j = pkg_index(t);
+        lk[t] = i < n ? F[min(i, 255)] << 1 : kMergeInf;
+        pk[t] = j >= 0 && j < np ? ((F[2 * j] + F[2 * j + 1]) << 1) | 1u : kMergeInf;  // level 1: pairs of the leaves
+    }
+    // entry e = k EPL + s (level 0: no packages) in lane e & 63 of register e >> 6
+    uint32_t mlo[2] = {0u, 0u}, mhi[2] = {0u, 0u}, mcum[2] = {0u, 0u};
+    // the gather's source (see below): lane 2 (31 - (lane & 31)), upper-half slot t's
+    // packages from slot EPL - 1 - 2t - (lane >> 5)
+    const int src = 8 * (31 - (lane & 31));
+    for (int k = 1; k < kTailLevels; ++k) {
+        uint32_t x[EPL];
+        if constexpr (EPL == 1) {
+            x[0] = lane < 32 ? lk[0] : pk[0];
+        } else {
+#pragma unroll
+            for (int t = 0; t < H; ++t) {
+                x[t] = lk[t];
+                x[H + t] = pk[t];
+            }
+        }
+        merge_bitonic<EPL>(x);
+        int before = 0;
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) {
+            const unsigned long long m = __ballot((x[s] & 1u) != 0u);
+            const int e = k * EPL + s;
+            const bool here = lane == (e & 63);
+            if (EPL < 8 || e < 64) {  // (uniform)
+                mlo[0] = here ? (uint32_t)m : mlo[0];
+                mhi[0] = here ? (uint32_t)(m >> 32) : mhi[0];
+                mcum[0] = here ? (uint32_t)before : mcum[0];
+            } else {
+                mlo[1] = here ? (uint32_t)m : mlo[1];
+                mhi[1] = here ? (uint32_t)(m >> 32) : mhi[1];
+                mcum[1] = here ? (uint32_t)before : mcum[1];
+            }
+            before += __popcll(m);
+        }
+        // the next level's packages: pairs (2j, 2j + 1) -- neighbouring lanes of a
+        // slot -- summed in the even lane, then gathered to their descending places
+        const int npn = (n + np) >> 1;
+        uint32_t q[EPL];
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) q[s] = (x[s] >> 1) + (lane_xor<1>(x[s]) >> 1);
+#pragma unroll
+        for (int t = 0; t < H; ++t) {
+            uint32_t v;
+            if constexpr (EPL == 1) {
+                v = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)q[0]);
+            } else {
+                const uint32_t vh = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)q[EPL - 1 - 2 * t]);
+                const uint32_t vl = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)q[EPL - 2 - 2 * t]);
+                v = (lane & 32) ? vl : vh;
+            }
+            const int j = pkg_index(t);
+            pk[t] = j >= 0 && j < npn ? (v << 1) | 1u : kMergeInf;
+        }
+        np = npn;
+    }
+    // the solution, deepest level first: the prefix of level k holds 2 * (packages
+    // taken at level k+1) items, the packages among them are the ones taken at level
+    // k-1 (every lane computes it: uniform values)
+    int packages = n - 1;
+#pragma unroll
+    for (int k = kTailLevels - 1; k >= 0; --k) {
+        const int cc = max(2 * packages, 0);  // <= 2n - 2 < 64 EPL
+        const int e = k * EPL + (cc >> 6), b = cc & 63;
+        uint32_t lo, hi, cm;
+        if (EPL < 8 || e < 64) {
+            lo = (uint32_t)__builtin_amdgcn_readlane((int)mlo[0], e);
+            hi = (uint32_t)__builtin_amdgcn_readlane((int)mhi[0], e);
+            cm = (uint32_t)__builtin_amdgcn_readlane((int)mcum[0], e);
+        } else {
+            lo = (uint32_t)__builtin_amdgcn_readlane((int)mlo[1], e - 64);
+            hi = (uint32_t)__builtin_amdgcn_readlane((int)mhi[1], e - 64);
+            cm = (uint32_t)__builtin_amdgcn_readlane((int)mcum[1], e - 64);
+        }
+        const unsigned long long m = (((unsigned long long)hi << 32) | lo) & ((1ull << b) - 1ull);
+        const int pkc = (int)cm + __popcll(m);
+        leaf[k] = cc - pkc;
+        packages = pkc;
+    }
+}
+
+// rank of every present key among the n keys (the stable ascending sort by
+// frequency, symbol_counting.rs:92-94: ties by symbol, which the key's low byte
+// carries); leaf rank -> F (frequency), Sym.  NS key slots per lane (key i at lane
+// i % 64, slot i / 64); the keys read eight at a time, loads together; K: u32 keys
+// (frequency << 8 | s) when every frequency is below 2^24, else u64.
+template <int NS, typename K>
+__device__ __forceinline__ void tail_rank(const K* Key, int n, uint32_t* F, uint8_t* Sym) {
+    const int lane = lane_id();
+    K mk[NS];
+    uint32_t rk[NS];
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+        mk[r] = lane + 64 * r < n ? Key[lane + 64 * r] : (K)~(K)0;
+        rk[r] = 0u;
+    }
+    constexpr int V = 16 / sizeof(K);  // keys per 16-byte read
+    int j = 0;
+    for (; j + 4 * V <= n; j += 4 * V) {
+        K kk[4 * V];
+#pragma unroll
+        for (int u = 0; u < 4 * V; ++u) kk[u] = Key[j + u];
+#pragma unroll
+        for (int u = 0; u < 4 * V; ++u)
+#pragma unroll
+            for (int r = 0; r < NS; ++r) rk[r] += kk[u] < mk[r] ? 1u : 0u;
+    }
+    for (; j < n; ++j) {
+        const K kk = Key[j];
+#pragma unroll
+        for (int r = 0; r < NS; ++r) rk[r] += kk < mk[r] ? 1u : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < NS; ++r)
+        if (lane + 64 * r < n) {
+            F[rk[r]] = (uint32_t)(mk[r] >> 8);
+            Sym[rk[r]] = (uint8_t)mk[r];
+        }
+}
+
+template <typename K>
+__device__ __forceinline__ void tail_rank_any(const K* Key, int n, uint32_t* F, uint8_t* Sym) {
+    const int ns = (n + 63) >> 6;  // (uniform in the wave)
+    if (ns <= 1)
+        tail_rank<1>(Key, n, F, Sym);
+    else if (ns == 2)
+        tail_rank<2>(Key, n, F, Sym);
+    else
+        tail_rank<4>(Key, n, F, Sym);
+}
+
+__device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_hist, const uint32_t* dc_hist, int frame,
+                                            const Geom& g, uint32_t* __restrict__ code_tab, uint8_t* __restrict__ out,
+                                            size_t out_stride, uint32_t* __restrict__ hdr_len,
+                                            const uint8_t* __restrict__ qtab_u8, int bits_per_channel,
+                                            int* __restrict__ status, int* sCnt, int* sBits) {
+    const int lane = lane_id(), tab = threadIdx.x >> 6;
+    const bool ac = tab & 1;
+    const int c = tab >> 1;
+    const int cap = ac ? 256 : 16;
+    uint8_t* const base = lds + kTailBase[tab];
+    uint32_t* const F = reinterpret_cast<uint32_t*>(base);
+    unsigned long long* const Key = reinterpret_cast<unsigned long long*>(F + cap);
+    uint32_t* const Key32 = F + cap;  // (the same region)
+    uint8_t* const Sym = reinterpret_cast<uint8_t*>(F + 3 * cap);
+    int* const bits16 = sBits + 16 * tab;
+
+    // ---- 1 (AC: symbols lane + 64 q; DC: symbol lane < 16 -- coalesced loads)
+    uint32_t f[4] = {0u, 0u, 0u, 0u};
+    if (ac) {
+        const uint32_t* h = ac_hist + ((size_t)frame * kHistReps * 2 + c) * 256 + lane;
+#pragma unroll
+        for (int r = 0; r < kHistReps; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) f[q] += ld_agent(h + (size_t)r * 512 + 64 * q);
+    } else if (lane < 16) {
+        const uint32_t* h = dc_hist + (size_t)frame * kHistReps * 32 + c * 16 + lane;
+#pragma unroll
+        for (int r = 0; r < kHistReps; ++r) f[0] += ld_agent(h + (size_t)r * 32);
+    }
+    // keys (frequency << 8 | symbol): u32 while every frequency is below 2^24
+    const bool k32 = __ballot(((f[0] | f[1] | f[2] | f[3]) >> 24) != 0u) == 0ull;
+    // present symbols compacted slot by slot (order is immaterial: the keys carry
+    // their symbols)
+    uint32_t* const ct = code_tab + ((size_t)frame * 4 + tab) * 256;
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int sym = lane + 64 * q;
+        const bool p = f[q] > 0u;
+        const unsigned long long bm = __ballot(p);
+        const int at = n + __popcll(bm & ((1ull << lane) - 1ull));
+        if (p) {
+            if (k32)
+                Key32[at] = (f[q] << 8) | (unsigned)sym;
+            else
+                Key[at] = ((unsigned long long)f[q] << 8) | (unsigned)sym;
+        } else {
+            ct[sym] = 0;  // (a present symbol's entry: phase 5)
+        }
+        n += __popcll(bm);
+    }
+    // k_tables' checks: a table without symbols; symbol 0xFF in an AC table (the
+    // reference's lookup table has 255 entries)
+    raise_status(status, ((lane == 0 && n == 0) || (ac && lane == 63 && f[3] > 0u)) ? 2 : 0);  // (s 255: lane 63, q 3)
+    if (lane == 0) sCnt[tab] = n;  // (read by every wave in phase 6, after the barrier)
+    if (lane < 16) bits16[lane] = 0;
+    wave_lds_sync();
+
+#if DMMT_TAIL_STOP == 1  // study: the tail's phases timed by truncation
+    return;
+#endif
+    // ---- 2: rank = present keys below mine (key i at lane i % 64, slot i / 64)
+    if (k32)
+        tail_rank_any(Key32, n, F, Sym);
+    else
+        tail_rank_any(Key, n, F, Sym);
+    wave_lds_sync();
+
+#if DMMT_TAIL_STOP == 2  // study: the tail's phases timed by truncation
+    return;
+#endif
+    // ---- 3, 4 (wave-uniform choice of the merge width)
+    int leaf[kTailLevels];
+    if (n <= 32)
+        tail_levels<1>(F, n, leaf);
+    else if (n <= 64)
+        tail_levels<2>(F, n, leaf);
+    else if (n <= 128)
+        tail_levels<4>(F, n, leaf);
+    else
+        tail_levels<8>(F, n, leaf);
+
+#if DMMT_TAIL_STOP == 3  // study: the tail's phases timed by truncation
+    return;
+#endif
+    uint32_t len[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = lane + 64 * r;
+        len[r] = 0;
+        if (i < n) {
+            uint32_t L = i == 0 ? 1u : 0u;
+#pragma unroll
+            for (int k = 0; k < kTailLevels; ++k) L += i < leaf[k] ? 1u : 0u;
+            len[r] = L;
+            atomicAdd(&bits16[L - 1], 1);
+        }
+    }
+
+    // ---- 5: code(rank i) = sum over the ranks above i of 2^(16 - len), mod 2^16
+    {
+        uint32_t carry = 0;
+        uint32_t inc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t wgt = len[r] ? 1u << (16 - len[r]) : 0u;
+            inc[r] = carry + wave_incl_scan_full_u32(wgt);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)inc[r], 63);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = lane + 64 * r;
+            if (i < n) {
+                const uint32_t pat = (carry - inc[r]) & 0xFFFFu;  // left aligned u16 (wrapping as in the reference)
+                ct[Sym[i]] = (len[r] << 16) | (pat >> (16 - len[r]));
+            }
+        }
+    }
+    __syncthreads();  // every table's count (sCnt); this wave's BITS
+
+#if DMMT_TAIL_STOP == 5  // study: the tail's phases timed by truncation
+    return;
+#endif
+    // ---- 6
+    const int nt[4] = {sCnt[0], sCnt[1], sCnt[2], sCnt[3]};
+    write_table_header(out + (size_t)frame * out_stride, tab, lane, 64, n, nt, Sym, bits16, g, qtab_u8,
+                       bits_per_channel, hdr_len + frame);
 }
 
 // ============================================================== operator: DCT only
@@ -1138,18 +1500,29 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
     return hipGetLastError();
 }
 
-hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st) {
+// The fused tail counts in 32 bits: a frame's symbols (at most 64 per block) times
+// the 15 levels a package can sum over stay below 2^30 (a key weight << 1 | tag
+// stays below its merge's padding); stripes keep k_tables
+// (their histograms are summed on the host first)
+bool tables_fusable(const Geom& g) { return g.stripe_first && !g.more_after && g.bpf * 64 * 16 < (1ll << 30); }
+
+hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st, bool fuse_tables,
+                       int bits_per_channel, uint8_t* out, size_t out_stride) {
     // at most 1024 workgroups (4K: 1.5 blocks per thread): fewer histogram
     // flushes; 4K q90 bench 157.5 -> 159.6 Gpx/s, 8K 4:2:0 296.6 -> 299.0 against
     // one block per thread (512: faster pipelined still, but k_hist alone +4 us)
     const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
+    const bool fuse = fuse_tables && tables_fusable(g);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g, w.ac_hist,
+                           w.dc_hist, w.status, w.arrive, w.code_tab, out, out_stride, w.hdr_len, w.qtab_u8,
+                           bits_per_channel);
+    };
     if (check_cat)
-        hipLaunchKernelGGL(k_hist<true>, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g,
-                           w.ac_hist, w.dc_hist, w.status);
+        fuse ? go(k_hist<true, true>) : go(k_hist<true, false>);
     else
-        hipLaunchKernelGGL(k_hist<false>, grid, dim3(256), 0, st, (const int16_t*)w.coef, w.dcdiff, w.lastnz, g,
-                           w.ac_hist, w.dc_hist, w.status);
+        fuse ? go(k_hist<false, true>) : go(k_hist<false, false>);
     return hipGetLastError();
 }
 

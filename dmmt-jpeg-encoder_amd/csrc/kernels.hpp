@@ -36,7 +36,12 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
                         const Work& w, hipStream_t st);
 // DC differences, AC and DC histograms, last non-zero positions of the blocks in
 // w.coef (check_cat: an AC -32768, which has no category, can occur)
-hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st);
+// fuse_tables: when tables_fusable(g), the frame's last k_hist workgroup also does
+// launch_tables' work (code tables, header into out), and no launch_tables follows
+bool tables_fusable(const Geom& g);
+hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st,
+                       bool fuse_tables = false, int bits_per_channel = 8, uint8_t* out = nullptr,
+                       size_t out_stride = 0);
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st);
 // fuse_offsets: when offsets_fusable(g), k_emit's last workgroup per frame also

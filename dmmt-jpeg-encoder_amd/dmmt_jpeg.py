@@ -102,6 +102,7 @@ def lib():
     L.dmmt_decode_ppm_device.argtypes = [vp, vp, sz, P(DmmtPpmHeader), vp, vp]
     L.dmmt_convert_ppm_device_batch.argtypes = [vp, P(DmmtPpmFile), i32, P(DmmtOptions), P(i32)]
     L.dmmt_ctx_batch_redone.argtypes = [vp]
+    L.dmmt_ctx_check_device.argtypes = [vp, P(i32)]
     L.dmmt_free.argtypes = [vp]
     L.dmmt_free.restype = None
     L.dmmt_strerror.argtypes = [ctypes.c_int]
@@ -360,6 +361,14 @@ class Encoder:
 
     def num_devices(self) -> int:
         return lib().dmmt_ctx_num_devices(self._ctx)
+
+    def check_device(self) -> int:
+        """dmmt_ctx_check_device: the context's GPU is the working thread's device and
+        every pooled buffer lies on it (every member, on its own thread, for a
+        multi-GPU context); returns the (first) device id"""
+        d = ctypes.c_int32(-1)
+        _check(lib().dmmt_ctx_check_device(self._ctx, ctypes.byref(d)), "check_device")
+        return int(d.value)
 
     def member(self, i: int) -> int:
         """member context i's handle (borrowed: valid while this context lives)"""

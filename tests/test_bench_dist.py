@@ -47,6 +47,9 @@ class StandInEncoder:
     def synchronize(self):
         pass
 
+    def check_device(self):
+        return self.rank
+
     def set_lanes(self, n):
         self.log.append(("lanes", self.rank, n))
 
@@ -106,6 +109,14 @@ def test_bench_two_ranks_gloo(tmp_path):
     expect = w * h * fps * 20 * world / (line["ms_per_step"] * 20 / 1e3) / 1e6
     assert line["value"] == pytest.approx(expect, rel=2e-3)
     assert line["config"]["parallelism"] == "independent frames x2"
+    # the line validates itself: each rank's own time and rate, its device, the world
+    ranks = line["config"]["ranks"]
+    assert ranks["world_size"] == 2 and ranks["backend"] == "gloo" and ranks["devices"] == [0, 1]
+    assert ranks["one_device_per_rank"] and max(ranks["seconds"]) == pytest.approx(line["ms_per_step"] * 20 / 1e3,
+                                                                                   rel=1e-3)
+    assert ranks["seconds"][1] > ranks["seconds"][0] * 0.99  # (barrier-bracketed: the slow rank bounds both)
+    for sec, rate in zip(ranks["seconds"], ranks["mpixel_s"]):
+        assert rate == pytest.approx(w * h * fps * 20 / sec / 1e6, rel=1e-3)
 
 
 def test_bench_line_fields_single_rank(monkeypatch):

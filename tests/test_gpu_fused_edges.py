@@ -1,0 +1,127 @@
+"""The edges of the two "last arriver does the rest" fusions, byte for byte against
+the oracle.
+
+* k_emit's fused chunk offsets: rounds of kFusedRoundChunks = 1536
+  chunks, at most kFusedOffsetsMaxChunks = 6144 chunks per frame (k_offsets
+  above).  Frames of exactly 1536 and 1537 chunks (one round, a carry into a
+  second), 6144 (four rounds, the largest fused frame) and just above 6144 (the
+  k_offsets launch), alone, in multi-frame launches (per-frame arrival counters,
+  32-bit carries per frame) and with restart intervals (segmented scans).
+  [binary_stream.rs:38-96, segment_marker_injector.rs:13-30: the bytes those
+  offsets place]
+* k_hist's fused Huffman tables (tables_tail): frames up to tables_fusable's
+  bound take them; 1 to 3 frames per launch; the DMMT_FUSE_TABLES=0 build path
+  (k_tables) must give the same files.  [length_limited.rs:37-134,
+  symbol_counting.rs:55-94, huffman/encoder.rs:45-157, encoder.rs:125-262]"""
+import concurrent.futures as cf
+import os
+
+import numpy as np
+import pytest
+
+import dmmt_jpeg
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+CPU_THREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+def _opts(sub, q, ri=0):
+    luma, chroma = dmmt_jpeg.quality_tables(q)
+    return dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
+                                              chroma_table=chroma, restart_interval=ri)
+
+
+def _chunks(w, h, sub):
+    hr, vr = (1, 1) if sub == 0 else ((2, 1) if sub == 1 else (2, 2))
+    mcus = -(-w // (8 * hr)) * -(-h // (8 * vr))
+    return -(-mcus * (hr * vr + 2) // 256)
+
+
+def _encode_device(enc, w, h, n, opts, first=0):
+    d = enc.malloc(w * h * 3 * n)
+    stride = (dmmt_jpeg.max_jpeg_bytes(w, h, int(opts.chroma_subsampling_preset)) + 255) // 256 * 256
+    d_out, d_len = enc.malloc(stride * n), enc.malloc(4 * n)
+    try:
+        enc.fill_synthetic(d, w, h, n, first_frame=first)
+        host = np.frombuffer(enc.d2h(d, w * h * 3 * n), np.uint8).reshape(n, h, w, 3)
+        enc.encode_device(d, n, w, h, opts, d_out, stride, d_len)
+        enc.synchronize()
+        lens = np.frombuffer(enc.d2h(d_len, 4 * n), np.uint32)
+        return host, [enc.d2h(d_out + i * stride, int(lens[i])) for i in range(n)]
+    finally:
+        for p in (d, d_out, d_len):
+            enc.free(p)
+
+
+def _oracle_all(frames, sub, opts):
+    luma, chroma = list(opts.luma_table), list(opts.chroma_table)
+    ri = opts.restart_interval
+    with cf.ThreadPoolExecutor(min(len(frames), 4)) as ex:
+        return list(ex.map(lambda f: oracle.encode(f, 255, sub, luma, chroma, restart_interval=ri,
+                                                   threads=max(1, CPU_THREADS // len(frames)), parallel=True), frames))
+
+
+@pytest.mark.parametrize("w,h,sub,nch", [
+    (4096, 2048, 0, 1536),   # one round, exactly full
+    (2400, 3496, 0, 1537),   # the carry into a second round
+    (8192, 8192, 2, 6144),   # four rounds: the largest fused frame
+    (8192, 8208, 2, 6156),   # above: k_offsets
+])
+def test_fused_offsets_round_edges(encoder, w, h, sub, nch):
+    assert _chunks(w, h, sub) == nch
+    opts = _opts(sub, 90)
+    host, gpu = _encode_device(encoder, w, h, 1, opts, first=nch)
+    assert gpu == _oracle_all(list(host), sub, opts)
+
+
+@pytest.mark.parametrize("nf", [2, 3])
+def test_fused_offsets_multi_frame_launch(encoder, nf):
+    """nf frames of 1537 chunks in one launch: every frame's own counters and carries"""
+    opts = _opts(0, 75)
+    host, gpu = _encode_device(encoder, 2400, 3496, nf, opts, first=7)
+    assert gpu == _oracle_all(list(host), 0, opts)
+
+
+@pytest.mark.parametrize("ri", [1, 37, 300])
+def test_fused_offsets_restart_segments(encoder, ri):
+    """restart intervals: the chunk grid restarts per segment and the scans are
+    segmented; 1537-chunk-class frame, two per launch"""
+    opts = _opts(0, 90, ri)
+    host, gpu = _encode_device(encoder, 2400, 3496, 2, opts, first=11)
+    assert gpu == _oracle_all(list(host), 0, opts)
+
+
+@pytest.mark.parametrize("w,h,sub", [(64, 48, 0), (1920, 1080, 2), (3840, 2160, 0), (333, 97, 1)])
+def test_fused_tables_match_k_tables(w, h, sub):
+    """the tables built in k_hist's last workgroup and by the k_tables launch
+    (DMMT_FUSE_TABLES=0 context): the same files, and the oracle's"""
+    opts = _opts(sub, 90)
+    outs = {}
+    for fuse in ("1", "0"):
+        os.environ["DMMT_FUSE_TABLES"] = fuse
+        try:
+            enc = dmmt_jpeg.Encoder(0)
+        finally:
+            os.environ.pop("DMMT_FUSE_TABLES")
+        try:
+            host, outs[fuse] = _encode_device(enc, w, h, 3, opts, first=w)
+        finally:
+            enc.close()
+    assert outs["1"] == outs["0"] == _oracle_all(list(host), sub, opts)
+
+
+def test_fused_tables_skewed_histograms(encoder):
+    """flat frames (one symbol dominates, others rare: the length limit of 15 binds)
+    and a noise frame (wide histograms, long codes) through the fused tables"""
+    rng = np.random.default_rng(3)
+    frames = [np.zeros((64, 96, 3), np.uint8), np.full((40, 40, 3), 200, np.uint8),
+              rng.integers(0, 256, (96, 128, 3), dtype=np.uint8)]
+    frames[0][5, 7] = 255
+    for sub in (0, 2):
+        for q in (1, 50, 100):
+            opts = _opts(sub, q)
+            for f in frames:
+                got = encoder.encode(dmmt_jpeg.Image.from_array(f), opts)
+                assert got == oracle.encode(f, 255, sub, list(opts.luma_table), list(opts.chroma_table))

@@ -56,6 +56,28 @@ def test_group_shape(group4):
         e.close()
 
 
+def test_members_on_their_devices(group4):
+    """dmmt_ctx_check_device after work on every member: each member's worker thread
+    runs on the member's GPU and every pooled buffer (lane workspaces, tables, the
+    group's staging) lies there -- the readiness check the group workers also run
+    before each member's part of a call (here all members are GPU 0)"""
+    rgb = synthetic(300, 260, frame=3)
+    img = dmmt_jpeg.Image.from_array(rgb)
+    ref = oracle.encode(rgb, 255, 2, *dmmt_jpeg.quality_tables(75))
+    assert group4.encode_striped(img, _opts(2, 75)) == ref
+    assert group4.encode_batch([img] * 5, _opts(2, 75)) == [ref] * 5
+    assert group4.check_device() == 0
+    for i in range(4):
+        assert _Member(group4.member(i)).check_device() == 0
+    e = dmmt_jpeg.Encoder(0)
+    try:
+        assert e.check_device() == 0  # before any buffer exists
+        assert e.encode(img, _opts(2, 75)) == ref
+        assert e.check_device() == 0
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("sub", [0, 1, 2])
 @pytest.mark.parametrize("shape", [(120, 200), (37, 53), (16, 16), (8, 5), (257, 129), (64, 64)])
 @pytest.mark.parametrize("ri_rows", [0, 1, 2])
