@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "device_common.hpp"
 #include "kernels.hpp"
 
@@ -470,6 +472,9 @@ struct FastLoads {
     unsigned long long rbase;
 };
 
+#ifndef DMMT_PPM_SHORT_FAST
+#define DMMT_PPM_SHORT_FAST 1  // (A/B builds: 0)
+#endif
 template <typename Out>
 __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* __restrict__ rep,
                                                           const uint32_t* __restrict__ counts,
@@ -541,6 +546,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         static_assert(P == 2, "the per-piece counts are scanned as two 16-bit fields");
         uint32_t st[P][4], sg[P][4], wnext[P];
         uint32_t n01 = 0;  // starts per piece, two 16-bit fields
+        uint32_t lm = 0;   // token starts followed by three more token bytes (tokens of 4+ bytes)
 #pragma unroll
         for (int q = 0; q < P; ++q) {
 #pragma unroll
@@ -558,11 +564,18 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
             }
             if (lane == 63) wnext[q] = sText[4 * (p + 1)];
             uint32_t nq = 0;
+            const uint32_t sgn = sig_bytes(wnext[q]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 st[q][k] = starts_of(sg[q][k], prev);
                 prev = sg[q][k];
                 nq += (uint32_t)__popc(st[q][k]);
+                // byte j of run4: bytes j .. j + 3 are all token bytes
+                if (!DMMT_PPM_SHORT_FAST) continue;
+                const uint32_t nb = k < 3 ? sg[q][k + 1] : sgn, g = sg[q][k];
+                const uint32_t run4 = g & __builtin_amdgcn_alignbyte(nb, g, 1u) & __builtin_amdgcn_alignbyte(nb, g, 2u) &
+                                      __builtin_amdgcn_alignbyte(nb, g, 3u);
+                lm |= st[q][k] & run4;
             }
             n01 |= nq << (16 * q);
         }
@@ -599,27 +612,36 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         // token's entry is its first four bytes -- its digits and terminator, which the
         // thread of the token combines -- or, for a token of four or more bytes,
         // 0x80000000 | its chunk offset (its text is read back from global memory).
+        // A wave none of whose tokens has four bytes (lm: every 8-bit image without
+        // leading zeros) stores the four bytes without the test.
+        auto compact = [&](auto long_tokens) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const uint32_t off = 16u * (uint32_t)(tid + kPpmThreads * q);
-            uint32_t r = rank[q] + pad;
+            for (int q = 0; q < P; ++q) {
+                const uint32_t off = 16u * (uint32_t)(tid + kPpmThreads * q);
+                uint32_t r = rank[q] + pad;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t m = st[q][k];
-                if (m) {
-                    const uint32_t wn = k < 3 ? w[q][k + 1] : wnext[q];
-                    auto entry = [&](uint32_t a) {
-                        const uint32_t x = __builtin_amdgcn_alignbyte(wn, w[q][k], a);
-                        // no byte below '0' (whitespace) among the four: four or more bytes
-                        const bool lng = (((x | 0x80808080u) - 0x30303030u) & 0x80808080u) == 0x80808080u;
-                        return lng ? 0x80000000u | (off + 4 * k + a) : x;
-                    };
-                    sTok[r] = entry((uint32_t)__builtin_ctz(m) >> 3);
-                    if (m & (m - 1u)) sTok[r + 1] = entry((uint32_t)(31 - __clz((int)m)) >> 3);
-                    r += (uint32_t)__popc(m);
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t m = st[q][k];
+                    if (m) {
+                        const uint32_t wn = k < 3 ? w[q][k + 1] : wnext[q];
+                        auto entry = [&](uint32_t a) {
+                            const uint32_t x = __builtin_amdgcn_alignbyte(wn, w[q][k], a);
+                            if constexpr (!decltype(long_tokens)::value) return x;
+                            // no byte below '0' (whitespace) among the four: four or more bytes
+                            const bool lng = (((x | 0x80808080u) - 0x30303030u) & 0x80808080u) == 0x80808080u;
+                            return lng ? 0x80000000u | (off + 4 * k + a) : x;
+                        };
+                        sTok[r] = entry((uint32_t)__builtin_ctz(m) >> 3);
+                        if (m & (m - 1u)) sTok[r + 1] = entry((uint32_t)(31 - __clz((int)m)) >> 3);
+                        r += (uint32_t)__popc(m);
+                    }
                 }
             }
-        }
+        };
+        if (!DMMT_PPM_SHORT_FAST || __ballot(lm != 0u))  // (uniform)
+            compact(std::true_type{});
+        else
+            compact(std::false_type{});
         __syncthreads();
         // one thread per group of four tokens: the entries' digits (the text of a
         // token of four or more bytes is read back from global memory, its
