@@ -1065,9 +1065,6 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
 //  6 the DHT segment, and for table 0 the rest of the header (write_table_header)
 // One barrier: before 6 (every table's symbol count).  LDS per table (bytes):
 // F u32[cap] | the keys u64[cap] | Sym u8[cap]; cap = 256 for the AC tables, 16 DC.
-#ifndef DMMT_TAIL_STOP
-#define DMMT_TAIL_STOP 0
-#endif
 constexpr int kTailLevels = 15;
 constexpr int kTailBase[4] = {0, 208, 3536, 3744};
 static_assert(kTailBase[3] + 3328 == kTailLdsBytes, "tables_tail's LDS regions");
@@ -1289,9 +1286,6 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
     if (lane < 16) bits16[lane] = 0;
     wave_lds_sync();
 
-#if DMMT_TAIL_STOP == 1  // study: the tail's phases timed by truncation
-    return;
-#endif
     // ---- 2: rank = present keys below mine (key i at lane i % 64, slot i / 64)
     if (k32)
         tail_rank_any(Key32, n, F, Sym);
@@ -1299,9 +1293,6 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
         tail_rank_any(Key, n, F, Sym);
     wave_lds_sync();
 
-#if DMMT_TAIL_STOP == 2  // study: the tail's phases timed by truncation
-    return;
-#endif
     // ---- 3, 4 (wave-uniform choice of the merge width)
     int leaf[kTailLevels];
     if (n <= 32)
@@ -1313,9 +1304,6 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
     else
         tail_levels<8>(F, n, leaf);
 
-#if DMMT_TAIL_STOP == 3  // study: the tail's phases timed by truncation
-    return;
-#endif
     uint32_t len[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1351,9 +1339,6 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
     }
     __syncthreads();  // every table's count (sCnt); this wave's BITS
 
-#if DMMT_TAIL_STOP == 5  // study: the tail's phases timed by truncation
-    return;
-#endif
     // ---- 6
     const int nt[4] = {sCnt[0], sCnt[1], sCnt[2], sCnt[3]};
     write_table_header(out + (size_t)frame * out_stride, tab, lane, 64, n, nt, Sym, bits16, g, qtab_u8,

@@ -472,9 +472,6 @@ struct FastLoads {
     unsigned long long rbase;
 };
 
-#ifndef DMMT_PPM_SHORT_FAST
-#define DMMT_PPM_SHORT_FAST 1  // (A/B builds: 0)
-#endif
 template <typename Out>
 __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* __restrict__ rep,
                                                           const uint32_t* __restrict__ counts,
@@ -571,7 +568,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                 prev = sg[q][k];
                 nq += (uint32_t)__popc(st[q][k]);
                 // byte j of run4: bytes j .. j + 3 are all token bytes
-                if (!DMMT_PPM_SHORT_FAST) continue;
                 const uint32_t nb = k < 3 ? sg[q][k + 1] : sgn, g = sg[q][k];
                 const uint32_t run4 = g & __builtin_amdgcn_alignbyte(nb, g, 1u) & __builtin_amdgcn_alignbyte(nb, g, 2u) &
                                       __builtin_amdgcn_alignbyte(nb, g, 3u);
@@ -638,7 +634,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                 }
             }
         };
-        if (!DMMT_PPM_SHORT_FAST || __ballot(lm != 0u))  // (uniform)
+        if (__ballot(lm != 0u))  // (uniform)
             compact(std::true_type{});
         else
             compact(std::false_type{});

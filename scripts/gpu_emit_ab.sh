@@ -1,7 +1,7 @@
 # Round-4 k_emit check: the k_emit-sensitive GPU tests on the product library,
 # then the 4-lane bench A/B of the product against library variants (lib_<v>),
 # then rocprof one-lane kernel stats of each.
-# usage: bash scripts/gpu_r04_emit.sh TAG "v1 v2" [R]
+# usage: bash scripts/gpu_emit_ab.sh TAG "v1 v2" [R]
 set -o pipefail
 export TMPDIR=/tmp
 T=$1; V=$2; R=${3:-2}

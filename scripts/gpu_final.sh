@@ -1,7 +1,7 @@
 # Round-4 closing measurements on one box: the round check (smoke, whole -m gpu
 # suite, default bench line, rocprof of it), the DESIGN §5 config sweep, and the
 # in-process multi-member leg (two members on GPU 0).
-# usage: bash scripts/gpu_r04_final.sh TAG
+# usage: bash scripts/gpu_final.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-r04_final}

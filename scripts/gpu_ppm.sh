@@ -1,6 +1,6 @@
 # Round-4 PPM ingest check: the PPM / CLI / convert GPU tests, the ppm_ingest
 # timing of bench.py (scripts/ppm_probe.py) and a rocprofv3 kernel profile of it.
-# usage: bash scripts/gpu_r04_ppm.sh TAG
+# usage: bash scripts/gpu_ppm.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-ppm}

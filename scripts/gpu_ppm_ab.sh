@@ -1,6 +1,6 @@
-# Round-4 PPM A/B: the PPM GPU tests on the product and on each variant, then
+# PPM A/B: the PPM GPU tests on the product and on each variant, then
 # scripts/ppm_probe.py timings (R repeats) of each.
-# usage: bash scripts/gpu_r04_ppmab.sh TAG "v1 v2" [R]
+# usage: bash scripts/gpu_ppm_ab.sh TAG "v1 v2" [R]
 set -o pipefail
 export TMPDIR=/tmp
 T=$1; V=$2; R=${3:-3}
