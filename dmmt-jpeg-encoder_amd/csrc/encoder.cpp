@@ -196,16 +196,17 @@ int sync_lanes(dmmt_ctx* c) {
 int upload_tables(dmmt_ctx* c, const dmmt_options* opt, int maxval, int sb, hipStream_t st) {
     int rc;
     if ((rc = ensure(c->qtab, 128 * sizeof(float)))) return rc;
-    if ((rc = ensure(c->qtab_u8, 128))) return rc;
-    uint8_t q[128];
+    if ((rc = ensure(c->qtab_u8, 256))) return rc;
+    uint8_t q[256];  // natural order, then the DQT bytes (zigzag order) k_hist's fused tail stores
     memcpy(q, opt->luma_q, 64);
     memcpy(q + 64, opt->chroma_q, 64);
+    for (int i = 0; i < 128; ++i) q[128 + i] = q[(i & 64) + kZigzag[i & 63]];
     if (!c->q_valid || memcmp(q, c->q_cached, 128) != 0) {
         if ((rc = sync_lanes(c))) return rc;  // no lane may still read the old tables
         float qf[128];
         for (int i = 0; i < 128; ++i) qf[i] = (float)q[i];
         HIP_TRY(hipMemcpyAsync(c->qtab.p, qf, sizeof qf, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(c->qtab_u8.p, q, 128, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(c->qtab_u8.p, q, 256, hipMemcpyHostToDevice, st));
         HIP_TRY(hipStreamSynchronize(st));
         memcpy(c->q_cached, q, 128);
         c->q_valid = true;

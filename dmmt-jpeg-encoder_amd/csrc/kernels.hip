@@ -743,10 +743,13 @@ __device__ __forceinline__ void put_be16(uint8_t* p, int v) {
 // first, i.e. symrank -- symbols by ascending frequency -- reversed) and, for table
 // 0, SOI, APP0, DQT x2, SOF0, [DRI], SOS (encoder.rs:125-262) and the header length;
 // a later stripe of an image (dmmt_stripe_*) writes no header.  Written by threads
-// t0, t0 + step, ... of the table (k_tables: 256 per table; k_hist's fused tail: 64).
+// t0, t0 + step, ... of the table (k_tables: 256 per table; k_hist's fused tail: 64,
+// whose table-0 wave passes the DQT bytes of zigzag position t0 already loaded:
+// dq = luma | chroma << 8, else -1).
 __device__ void write_table_header(uint8_t* o, int tab, int t0, int step, int n, const int nt[4],
                                    const uint8_t* symrank, const int* bits16, const Geom& g,
-                                   const uint8_t* __restrict__ qtab_u8, int bits_per_channel, uint32_t* hdr_len) {
+                                   const uint8_t* __restrict__ qtab_u8, int bits_per_channel, uint32_t* hdr_len,
+                                   int dq = -1) {
     if (!g.stripe_first) {  // a later stripe of an image: tables only, no header
         if (tab == 0 && t0 == 0) *hdr_len = 0;
         return;
@@ -809,6 +812,11 @@ __device__ void write_table_header(uint8_t* o, int tab, int t0, int step, int n,
         const uint8_t sos[14] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x01, 0x02, 0x23, 0x03, 0x23, 0x00, 0x3F, 0x00};
         for (int i = 0; i < 14; ++i) o[pos_sos + i] = sos[i];
         *hdr_len = (uint32_t)(pos_sos + 14);
+    }
+    if (dq >= 0) {
+        o[25 + t0] = (uint8_t)dq;
+        o[94 + t0] = (uint8_t)(dq >> 8);
+        return;
     }
     for (int s = t0; s < 128; s += step) {
         const int q = s >> 6, i = s & 63;
@@ -1049,10 +1057,12 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
 // 32 bits: the host fuses only frames whose symbol counts, and thus every package
 // weight (at most 15 times their sum), stay below 2^30.  The phases of k_tables:
 //  1 the 8 replicas summed (agent-scope loads after the arrival); symbol s = lane
-//    + 64 q; present symbols compacted as keys (frequency << 8 | s), u32 when
-//    every frequency is below 2^24, else u64
-//  2 rank = present keys below mine (symbol_counting.rs:92-94's stable ascending
-//    sort over the f > 0 filter of 25-32)
+//    + 64 q; the present symbols counted
+//  2 symbol_counting.rs:92-94's stable ascending sort over the f > 0 filter of
+//    25-32: keys (frequency << 8 | s) sorted in registers (sort_bitonic,
+//    wave_merge.hpp; absent symbols are kMergeInf and sort last) when every
+//    frequency is below 2^24; else the 64-bit keys compacted and ranked
+//    (tail_rank)
 //  3 package-merge, limit 15 (length_limited.rs:37-134), in registers: level k is
 //    the merge of the leaves (ascending) with the pair sums of level k-1
 //    (ascending), ties leaf first -- keys (weight << 1 | is_package), one
@@ -1240,7 +1250,6 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
     uint8_t* const base = lds + kTailBase[tab];
     uint32_t* const F = reinterpret_cast<uint32_t*>(base);
     unsigned long long* const Key = reinterpret_cast<unsigned long long*>(F + cap);
-    uint32_t* const Key32 = F + cap;  // (the same region)
     uint8_t* const Sym = reinterpret_cast<uint8_t*>(F + 3 * cap);
     int* const bits16 = sBits + 16 * tab;
 
@@ -1257,40 +1266,60 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
 #pragma unroll
         for (int r = 0; r < kHistReps; ++r) f[0] += ld_agent(h + (size_t)r * 32);
     }
+    // table 0's wave: its lane's DQT bytes (zigzag position lane of both tables, kept
+    // in zigzag order by the host), loaded with the histograms rather than after
+    // the tables
+    int dq = -1;
+    if (tab == 0 && g.stripe_first) dq = (int)qtab_u8[128 + lane] | ((int)qtab_u8[192 + lane] << 8);
     // keys (frequency << 8 | symbol): u32 while every frequency is below 2^24
     const bool k32 = __ballot(((f[0] | f[1] | f[2] | f[3]) >> 24) != 0u) == 0ull;
-    // present symbols compacted slot by slot (order is immaterial: the keys carry
-    // their symbols)
     uint32_t* const ct = code_tab + ((size_t)frame * 4 + tab) * 256;
     int n = 0;
+    unsigned long long pres[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const int sym = lane + 64 * q;
-        const bool p = f[q] > 0u;
-        const unsigned long long bm = __ballot(p);
-        const int at = n + __popcll(bm & ((1ull << lane) - 1ull));
-        if (p) {
-            if (k32)
-                Key32[at] = (f[q] << 8) | (unsigned)sym;
-            else
-                Key[at] = ((unsigned long long)f[q] << 8) | (unsigned)sym;
-        } else {
-            ct[sym] = 0;  // (a present symbol's entry: phase 5)
-        }
-        n += __popcll(bm);
+        pres[q] = __ballot(f[q] > 0u);
+        if (f[q] == 0u) ct[lane + 64 * q] = 0;  // (a present symbol's entry: phase 5)
+        n += __popcll(pres[q]);
     }
     // k_tables' checks: a table without symbols; symbol 0xFF in an AC table (the
     // reference's lookup table has 255 entries)
     raise_status(status, ((lane == 0 && n == 0) || (ac && lane == 63 && f[3] > 0u)) ? 2 : 0);  // (s 255: lane 63, q 3)
     if (lane == 0) sCnt[tab] = n;  // (read by every wave in phase 6, after the barrier)
     if (lane < 16) bits16[lane] = 0;
-    wave_lds_sync();
 
-    // ---- 2: rank = present keys below mine (key i at lane i % 64, slot i / 64)
-    if (k32)
-        tail_rank_any(Key32, n, F, Sym);
-    else
+    // ---- 2: the present keys in ascending order (absent symbols: kMergeInf, last)
+    // -> F (frequency), Sym by leaf rank
+    if (k32) {
+        if (ac) {
+            uint32_t x[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = f[q] ? (f[q] << 8) | (uint32_t)(lane + 64 * q) : kMergeInf;
+            sort_bitonic<4>(x);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (lane + 64 * q < n) {
+                    F[lane + 64 * q] = x[q] >> 8;
+                    Sym[lane + 64 * q] = (uint8_t)x[q];
+                }
+        } else {
+            uint32_t x[1] = {f[0] ? (f[0] << 8) | (uint32_t)lane : kMergeInf};
+            sort_bitonic<1>(x);
+            if (lane < n) {
+                F[lane] = x[0] >> 8;
+                Sym[lane] = (uint8_t)x[0];
+            }
+        }
+    } else {  // rank among 64-bit keys, compacted slot by slot (order immaterial: the keys carry their symbols)
+        int at = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (f[q]) Key[at + __popcll(pres[q] & ((1ull << lane) - 1ull))] = ((unsigned long long)f[q] << 8) | (unsigned)(lane + 64 * q);
+            at += __popcll(pres[q]);
+        }
+        wave_lds_sync();
         tail_rank_any(Key, n, F, Sym);
+    }
     wave_lds_sync();
 
     // ---- 3, 4 (wave-uniform choice of the merge width)
@@ -1342,7 +1371,7 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
     // ---- 6
     const int nt[4] = {sCnt[0], sCnt[1], sCnt[2], sCnt[3]};
     write_table_header(out + (size_t)frame * out_stride, tab, lane, 64, n, nt, Sym, bits16, g, qtab_u8,
-                       bits_per_channel, hdr_len + frame);
+                       bits_per_channel, hdr_len + frame, dq);
 }
 
 // ============================================================== operator: DCT only

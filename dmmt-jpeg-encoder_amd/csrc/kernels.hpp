@@ -27,7 +27,7 @@ struct Work {
     int* status;                    // error words (raise_status): bit k of the error kinds -> word k; 1 value>max, 2 table, 4 category range, 16 output capacity
     const float* norm_lut;          // maxval-normalisation table
     const float* qtab;              // [2][64] f32
-    const uint8_t* qtab_u8;         // [2][64]
+    const uint8_t* qtab_u8;         // [2][64] natural order, then [2][64] zigzag (the DQT bytes)
 };
 
 enum Stage { ST_FRONT = 0, ST_HIST, ST_TABLES, ST_EMIT, ST_OFFSETS, ST_STUFFWRITE, ST_COUNT };

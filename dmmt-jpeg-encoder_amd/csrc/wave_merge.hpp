@@ -1,6 +1,7 @@
 // wave_merge.hpp -- one wave64 merges two sorted sequences of u32 keys in registers
 // (a bitonic merger: no LDS, no barrier), for k_hist's fused Huffman tables (the
-// package-merge levels, length_limited.rs:37-134).
+// package-merge levels, length_limited.rs:37-134); and sorts up to 256 keys the
+// same way (sort_bitonic: the tables' symbols by frequency, symbol_counting.rs:92-94).
 //
 // Layout: S = 64 * EPL elements, element e in lane e & 63, register slot e >> 6
 // ("slot-major"); the first S/2 elements ascending, the last S/2 DESCENDING (a
@@ -116,6 +117,100 @@ __device__ __forceinline__ void merge_bitonic(uint32_t (&x)[EPL]) {
     clean_lanes<4, EPL>(x);
     clean_lanes<2, EPL>(x);
     clean_lanes<1, EPL>(x);
+}
+
+// ---- full sort (k_hist's fused tail, phase 2): 64 * E keys, element e in lane
+// e & 63 of slot e >> 6, sorted ascending in place.  Bitonic sort in the "flip"
+// form: for each size k = 2 .. 64 E the pair (i, i ^ (k - 1)) -- the lower index
+// keeps the min -- then half-cleaners k/4 .. 1 as in merge_bitonic.
+
+// the value of lane (lane ^ M) for M = 2^j - 1
+template <int M>
+__device__ __forceinline__ uint32_t lane_flip(uint32_t x) {
+    if constexpr (M == 1) {
+        return lane_xor<1>(x);
+    } else if constexpr (M == 3) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x1B, 0xF, 0xF, false);  // quad_perm [3,2,1,0]
+    } else if constexpr (M == 7) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    } else if constexpr (M == 15) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    } else if constexpr (M == 31) {
+        return lane_xor<16>((uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));
+    } else {
+        static_assert(M == 63, "lane_flip: M in 1, 3, 7, 15, 31, 63");
+        return lane_reverse(x);
+    }
+}
+
+template <int M, int E>
+__device__ __forceinline__ void flip_lanes(uint32_t (&x)[E]) {
+    const bool upper = (threadIdx.x & ((M + 1) >> 1)) != 0;
+#pragma unroll
+    for (int s = 0; s < E; ++s) {
+        const uint32_t y = lane_flip<M>(x[s]);
+        x[s] = upper ? max(x[s], y) : min(x[s], y);
+    }
+}
+
+// slots a < b at size 128 or 256: element (a, l) against (b, 63 - l)
+__device__ __forceinline__ void flip_slots(uint32_t& a, uint32_t& b) {
+    const uint32_t r = lane_reverse(b);
+    const uint32_t lo = min(a, r), hi = max(a, r);
+    a = lo;
+    b = lane_reverse(hi);
+}
+
+template <int E>
+__device__ __forceinline__ void sort_bitonic(uint32_t (&x)[E]) {
+    static_assert(E == 1 || E == 2 || E == 4, "64, 128 or 256 keys");
+    flip_lanes<1>(x);
+    flip_lanes<3>(x);
+    clean_lanes<1>(x);
+    flip_lanes<7>(x);
+    clean_lanes<2>(x);
+    clean_lanes<1>(x);
+    flip_lanes<15>(x);
+    clean_lanes<4>(x);
+    clean_lanes<2>(x);
+    clean_lanes<1>(x);
+    flip_lanes<31>(x);
+    clean_lanes<8>(x);
+    clean_lanes<4>(x);
+    clean_lanes<2>(x);
+    clean_lanes<1>(x);
+    flip_lanes<63>(x);
+    clean_swap<16>(x);
+    clean_lanes<8>(x);
+    clean_lanes<4>(x);
+    clean_lanes<2>(x);
+    clean_lanes<1>(x);
+    if constexpr (E >= 2) {  // size 128
+#pragma unroll
+        for (int s = 0; s < E; s += 2) flip_slots(x[s], x[s + 1]);
+        clean_swap<32>(x);
+        clean_swap<16>(x);
+        clean_lanes<8>(x);
+        clean_lanes<4>(x);
+        clean_lanes<2>(x);
+        clean_lanes<1>(x);
+    }
+    if constexpr (E >= 4) {  // size 256
+        flip_slots(x[0], x[3]);
+        flip_slots(x[1], x[2]);
+#pragma unroll
+        for (int s = 0; s < 4; s += 2) {  // distance 64: slots (0, 1), (2, 3)
+            const uint32_t a = x[s], b = x[s + 1];
+            x[s] = min(a, b);
+            x[s + 1] = max(a, b);
+        }
+        clean_swap<32>(x);
+        clean_swap<16>(x);
+        clean_lanes<8>(x);
+        clean_lanes<4>(x);
+        clean_lanes<2>(x);
+        clean_lanes<1>(x);
+    }
 }
 
 }  // namespace dmmt

@@ -125,3 +125,24 @@ def test_fused_tables_skewed_histograms(encoder):
             for f in frames:
                 got = encoder.encode(dmmt_jpeg.Image.from_array(f), opts)
                 assert got == oracle.encode(f, 255, sub, list(opts.luma_table), list(opts.chroma_table))
+
+
+@pytest.mark.timeout(300)
+def test_fused_tables_u64_keys(encoder):
+    """A symbol counted 2^24 times or more: the fused tail ranks that table with
+    64-bit keys (phase 1's u32 keys need every frequency below 2^24) and the others
+    with 32-bit ones -- the back half from crafted blocks: 4:2:0, 267,264 luma
+    blocks whose 63 AC coefficients are all 1 (the symbol 0x01 counted 16,837,632
+    times), every 97th block noise, still within tables_fusable's bound."""
+    w, h, sub = 4096, 4176, 2
+    mcus = (w // 16) * (h // 16)
+    rng = np.random.default_rng(24)
+    coef = np.ones((mcus * 6, 64), np.int16)
+    coef[:, 0] = 0
+    noisy = np.arange(0, coef.shape[0], 97)
+    coef[noisy] = rng.integers(-50, 51, (noisy.size, 64), dtype=np.int16)
+    assert (mcus * 4) * 63 >= 1 << 24 and coef.shape[0] * 64 * 16 < 1 << 30
+    luma, chroma = dmmt_jpeg.quality_tables(90)
+    opts = _opts(sub, 90)
+    ref = oracle.encode_coefficients(coef, w, h, sub, luma, chroma)
+    assert encoder.encode_coefficients(coef, w, h, opts) == ref

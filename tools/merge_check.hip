@@ -1,6 +1,7 @@
-// GPU check of csrc/wave_merge.hpp: the lane exchanges against __shfl, and the
-// wave's bitonic merger against std::merge on random runs -- the lower ascending,
-// the upper descending (duplicates, padding, every run length).  Prints the mismatch counts; exit 0 when none.
+// GPU check of csrc/wave_merge.hpp: the lane exchanges against __shfl, the wave's
+// bitonic merger against std::merge on random runs -- the lower ascending, the
+// upper descending (duplicates, padding, every run length) -- and the bitonic sort
+// against std::sort (random keys among INF padding, duplicates).  Prints the mismatch counts; exit 0 when none.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,6 +37,18 @@ __global__ void k_merge(const uint32_t* in, uint32_t* out) {
     uint32_t* q = out + (size_t)blockIdx.x * 64 * EPL;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) q[64 * s + threadIdx.x] = x[s];
+}
+
+template <int E>
+__global__ void k_sort(const uint32_t* in, uint32_t* out) {
+    uint32_t x[E];
+    const uint32_t* p = in + (size_t)blockIdx.x * 64 * E;
+#pragma unroll
+    for (int s = 0; s < E; ++s) x[s] = p[64 * s + threadIdx.x];
+    sort_bitonic<E>(x);
+    uint32_t* q = out + (size_t)blockIdx.x * 64 * E;
+#pragma unroll
+    for (int s = 0; s < E; ++s) q[64 * s + threadIdx.x] = x[s];
 }
 
 static uint64_t g = 88172645463325252ull;
@@ -76,6 +89,32 @@ static long long check_merge(int trials) {
     return bad;
 }
 
+template <int E>
+static long long check_sort(int trials) {
+    const int S = 64 * E;
+    std::vector<uint32_t> in((size_t)trials * S), want, got((size_t)trials * S);
+    for (int t = 0; t < trials; ++t) {
+        const int n = (int)(rnd() % (S + 1));  // present keys; the rest INF (absent symbols)
+        const uint32_t range = (t % 3 == 0) ? 8u : (t % 3 == 1 ? 1000u : 0x7FFFFFFFu);
+        for (int i = 0; i < S; ++i) in[(size_t)t * S + i] = i < n ? rnd() % range : kMergeInf;
+        for (int i = S - 1; i > 0; --i) std::swap(in[(size_t)t * S + i], in[(size_t)t * S + rnd() % (i + 1)]);
+    }
+    want = in;
+    for (int t = 0; t < trials; ++t) std::sort(want.begin() + (size_t)t * S, want.begin() + (size_t)(t + 1) * S);
+    uint32_t *d_in, *d_out;
+    (void)hipMalloc(&d_in, in.size() * 4);
+    (void)hipMalloc(&d_out, in.size() * 4);
+    (void)hipMemcpy(d_in, in.data(), in.size() * 4, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_sort<E>, dim3(trials), dim3(64), 0, 0, d_in, d_out);
+    (void)hipMemcpy(got.data(), d_out, got.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    long long bad = 0;
+    for (size_t i = 0; i < got.size(); ++i) bad += got[i] != want[i];
+    printf("sort E=%d (%d keys): %lld of %zu differ\n", E, S, bad, got.size());
+    return bad;
+}
+
 int main() {
     const int blocks = 64;
     std::vector<uint32_t> h(blocks * 64), hb(blocks * 64);
@@ -90,6 +129,7 @@ int main() {
     for (uint32_t v : hb) bad += v;
     printf("lane exchanges: %lld mismatches\n", bad);
     bad += check_merge<1>(2000) + check_merge<2>(2000) + check_merge<4>(2000) + check_merge<8>(2000);
+    bad += check_sort<1>(2000) + check_sort<2>(2000) + check_sort<4>(2000);
     printf(bad ? "FAIL\n" : "ok\n");
     return bad != 0;
 }
