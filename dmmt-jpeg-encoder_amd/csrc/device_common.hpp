@@ -249,6 +249,17 @@ __device__ __forceinline__ void arrive_acquire() {
 #endif
 }
 
+// A non-temporal 16-byte load, for data no kernel of the path reads again: k_front's
+// input pixels, so that they do not displace from the MALL the coefficients and
+// staging the next kernels re-read (4K q90, 4 lanes: +2 % at 200 steps,
+// profiles/r05_v12_nt_io_ab.txt; the same hint on k_emit's coefficient loads costs
+// 17 %, on k_stuffwrite's output stores nothing)
+typedef unsigned int dmmt_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16_nt(const void* p) {
+    const dmmt_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const dmmt_u32x4*>(p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+
 // a load of another workgroup's result (agent scope)
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -237,7 +237,7 @@ struct RawTile {
                 const int row = q / RC, j = q - (q / RC) * RC;
                 const uint8_t* r = tb + (size_t)((uint32_t)row * rowpitch);  // pointer arithmetic: stays global
                 const uint8_t* a = r - ((uint32_t)(uintptr_t)r & 15u) + 16u * (uint32_t)j;
-                v[i] = q < NCHUNK ? *reinterpret_cast<const uint4*>(a) : make_uint4(0u, 0u, 0u, 0u);
+                v[i] = q < NCHUNK ? ld16_nt(a) : make_uint4(0u, 0u, 0u, 0u);
             }
             return;
         }
@@ -253,7 +253,7 @@ struct RawTile {
             const long long c = start - misalign(fbase, start) + 16LL * j;  // frame-relative
             if (c >= start + rowbytes) continue;
             if (c >= 0 && c + 16 <= fbytes) {
-                v[i] = *reinterpret_cast<const uint4*>(fbase + c);
+                v[i] = ld16_nt(fbase + c);
             } else {
                 uint32_t w[4] = {0u, 0u, 0u, 0u};
                 for (int k = 0; k < 16; ++k)
