@@ -979,13 +979,13 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
         __syncthreads();
         const unsigned long long in_pass = nbytes - pos < (unsigned long long)kStuffPass ? nbytes - pos : kStuffPass;
         const uint32_t len = (uint32_t)in_pass + ffs;
-        const uint32_t end = delta + len;  // staged bytes [delta, end)
-        uint8_t* const oa = o - delta;     // 16-byte aligned
-        for (uint32_t b0 = 16u * (uint32_t)tid; b0 < end; b0 += 16u * 256u) {
-            if (b0 >= delta && b0 + 16u <= end) {
-                *reinterpret_cast<uint4*>(oa + b0) = *reinterpret_cast<const uint4*>(sOut + b0);
+        const uint32_t send = delta + len;  // staged bytes [delta, send)
+        uint8_t* const oa = o - delta;      // 16-byte aligned
+        for (uint32_t sb = 16u * (uint32_t)tid; sb < send; sb += 16u * 256u) {
+            if (sb >= delta && sb + 16u <= send) {
+                *reinterpret_cast<uint4*>(oa + sb) = *reinterpret_cast<const uint4*>(sOut + sb);
             } else {  // the pass's first and last 16-byte pieces: only its own bytes
-                for (uint32_t i = max(b0, delta); i < min(b0 + 16u, end); ++i) oa[i] = sOut[i];
+                for (uint32_t i = max(sb, delta); i < min(sb + 16u, send); ++i) oa[i] = sOut[i];
             }
         }
         o += len;

@@ -394,12 +394,12 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_count(PpmText t, uint32_t* 
         const int h = tid;
         uint32_t c = 0;
 #pragma unroll
-        for (int v = 0; v < NW; ++v) {
-            c += sRed[v][h];
+        for (int u = 0; u < NW; ++u) {
+            c += sRed[u][h];
 #pragma unroll
             for (int q = h * kFastPieces; q < (h + 1) * kFastPieces; ++q) {
-                const uint32_t pb = v ? (sL[v - 1] >> q) & 1u : (q ? (sL[NW - 1] >> (q - 1)) & 1u : before);
-                c -= (sF[v] >> q) & pb & 1u;
+                const uint32_t pb = u ? (sL[u - 1] >> q) & 1u : (q ? (sL[NW - 1] >> (q - 1)) & 1u : before);
+                c -= (sF[u] >> q) & pb & 1u;
             }
         }
         const long long k = (long long)blockIdx.x * kCountChunks + h;
