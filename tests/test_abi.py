@@ -269,3 +269,20 @@ def test_build_info_reports_no_sdwa_peephole(L):
     profiles/r03_kemit_fault_study.md); the library says so"""
     info = L.dmmt_build_info().decode()
     assert "-amdgpu-sdwa-peephole=false" in info and "gfx950" in info
+
+
+def test_no_64bit_op_reads_the_last_allocated_vgpr(L):
+    """the round-3 k_emit fault pattern (profiles/r03_kemit_fault_study.md, round 5):
+    a 64-bit shift whose shift amount is the last VGPR of its kernel's allocation
+    computed wrong bits on MI355X; no 64-bit VALU operation of the product library
+    reads that register (tools/last_vgpr_check.py, from the built code objects)"""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("last_vgpr_check", os.path.join(ROOT, "tools", "last_vgpr_check.py"))
+    chk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(chk)
+    hits, kernels = [], 0
+    for co in chk.code_objects(dmmt_jpeg.LIB_PATH):
+        h, n = chk.check_object(co)
+        hits += h
+        kernels += n
+    assert kernels >= 20 and not hits, hits

@@ -12,7 +12,11 @@ instruction, register and wait stays as the compiler emitted it, so a subset
 whose rewrite makes the output exact holds the faulting instruction.
 
     python tools/sdwa_bisect.py list                 # k_emit's SDWA instructions, numbered
-    python tools/sdwa_bisect.py build NAME SPEC      # SPEC: none | all | a:b[,c:d...] (indices)
+    python tools/sdwa_bisect.py build NAME SPEC [VGPRS [LDS [INIT]]]
+        SPEC: none | all | a:b[,c:d...] (indices), k:... in place (no spare
+        registers); VGPRS / LDS: k_emit's register count / LDS bytes in its
+        descriptor (no code change; '-' keeps it); INIT: VGPRs zeroed at the
+        kernel's entry, e.g. 1-71 or 1-18,37-54 (v0 holds the work-item ids)
     python tools/sdwa_bisect.py stage                # the python side the GPU run needs
 
 Outputs go to sdwa_study/ (git-ignored, travels to the GPU box):
@@ -66,8 +70,10 @@ def sdwa_lines(lines):
     return [i for i in range(a, b) if SDWA_RE.match(lines[i])]
 
 
-def rewrite(line):
-    """The plain form of one SDWA instruction (dst_sel:DWORD, UNUSED_PAD only)."""
+def rewrite(line, keep=False):
+    """The plain form of one SDWA instruction (dst_sel:DWORD, UNUSED_PAD only).
+    keep: no spare registers -- the destination VGPR takes the extracted source
+    (None when it cannot: a compare, or a destination that is also a source)."""
     ind, op, ops, mods = SDWA_RE.match(line).groups()
     mods = dict(m.split(":") for m in mods.split())
     assert mods.get("dst_sel", "DWORD") == "DWORD" and mods.get("dst_unused", "UNUSED_PAD") == "UNUSED_PAD", line
@@ -87,6 +93,12 @@ def rewrite(line):
             continue
         off, wid = SEL[sel]
         t = SPARE[k]
+        if keep:
+            others = [x[5:-1] if x.startswith("sext(") else x for j, x in enumerate(srcs) if j != k]
+            if not re.fullmatch(r"v\d+", dst) or dst in others or sum(mods.get(f"src{j}_sel", "DWORD") != "DWORD"
+                                                             for j in range(len(srcs))) != 1:
+                return None
+            t = dst
         out.append(f"{ind}v_bfe_{'i32' if sx else 'u32'} {t}, {reg}, {off}, {wid}")
         new.append(t)
     out.append(f"{ind}{op}_e64 {dst}, {', '.join(new)}")
@@ -105,30 +117,71 @@ def parse_spec(spec, n):
     return sel
 
 
-def patched_asm(spec):
+def parse_regs(init):
+    regs = []
+    for part in init.split(","):
+        a, _, b = part.partition("-")
+        regs += list(range(int(a), int(b or a) + 1))
+    assert all(1 <= r for r in regs)
+    return regs
+
+
+def patched_asm(spec, vgprs=None, lds=None, init=None):
     lines = device_asm()
+    ren = os.environ.get("SDWA_RENAME")  # "71:79": k_emit's v71 renamed (a register-placement control)
+    if ren:
+        f, t = ren.split(":")
+        a0, b0 = kemit_range(lines)
+        assert not any(re.search(rf"\bv{t}\b|v\[\d+:\d+\]", lines[i]) and re.search(rf"v\[\d+:{f}\]|v\[{f}:", lines[i])
+                       for i in range(a0, b0)), "renamed register inside a tuple"
+        code_end = next(i for i in range(a0, b0) if lines[i].strip().startswith(".section"))
+        lines = [re.sub(rf"\bv{f}\b", f"v{t}", l) if a0 <= i < code_end else l for i, l in enumerate(lines)]
+    sub = os.environ.get("SDWA_SUB")  # "old=>new": one exact k_emit instruction replaced (\n: several)
+    if sub:
+        f, t = sub.split("=>")
+        a0, b0 = kemit_range(lines)
+        hits = [i for i in range(a0, b0) if lines[i].strip() == f]
+        assert len(hits) == 1, (f, len(hits))
+        lines[hits[0]] = "\n".join("\t" + x for x in t.split("\\n"))
+        lines = "\n".join(lines).split("\n")
     idx = sdwa_lines(lines)
-    chosen = parse_spec(spec, len(idx))
-    rep = {idx[j]: rewrite(lines[idx[j]]) for j in chosen}
+    keep = spec.startswith("k:")  # rewrite in place, no spare registers (occupancy unchanged)
+    chosen = parse_spec(spec[2:] if keep else spec, len(idx))
+    rep = {idx[j]: rewrite(lines[idx[j]], keep) for j in chosen}
+    rep = {i: r for i, r in rep.items() if r is not None}
+    chosen = rep if keep else chosen
     a0, b0 = kemit_range(lines)
-    assert not any(re.search(r"\bv7[2-9]\b|v\[7[0-9]:|v\[[0-9]+:7[2-9]\]", lines[i]) for i in range(a0, b0)), "spare used"
+    assert keep or not chosen or not any(re.search(r"\bv7[2-9]\b|v\[7[0-9]:|v\[[0-9]+:7[2-9]\]", lines[i])
+                                         for i in range(a0, b0)), "spare used"
     out = []
     for i, l in enumerate(lines):
         out.extend(rep.get(i, [l]))
-    if chosen:  # two spare VGPRs for k_emit: descriptor and metadata
-        a, b = kemit_range(out)
+    if chosen and vgprs is None and not keep:
+        vgprs = 74  # two spare VGPRs for k_emit
+    if init:  # entry: zero the chosen VGPRs (their contents are otherwise what the last wave left)
+        e = next(i for i, l in enumerate(out) if l.startswith(KEMIT + ":")) + 1
+        out[e:e] = [f"\tv_mov_b32_e32 v{r}, 0" for r in parse_regs(init)]
+    a, b = kemit_range(out)
+    nm = next(i for i, l in enumerate(out) if l.strip() == f".name:           {KEMIT}")
+    if vgprs is not None:  # descriptor and metadata
         for i in range(a, b):  # (the kernel descriptor lies inside the function's range)
-            out[i] = out[i].replace(".amdhsa_next_free_vgpr 72", ".amdhsa_next_free_vgpr 74")
-            out[i] = out[i].replace(".amdhsa_accum_offset 72", ".amdhsa_accum_offset 76")
-        nm = next(i for i, l in enumerate(out) if l.strip() == f".name:           {KEMIT}")
+            out[i] = out[i].replace(".amdhsa_next_free_vgpr 72", f".amdhsa_next_free_vgpr {vgprs}")
+            out[i] = out[i].replace(".amdhsa_accum_offset 72", f".amdhsa_accum_offset {(vgprs + 3) & ~3}")
         vc = next(i for i in range(nm, len(out)) if out[i].strip().startswith(".vgpr_count:"))
         assert out[vc].strip() == ".vgpr_count:     72", out[vc]
-        out[vc] = out[vc].replace("72", "74")
+        out[vc] = out[vc].replace("72", str(vgprs))
+    if lds is not None:
+        for i in range(a, b):
+            out[i] = out[i].replace(".amdhsa_group_segment_fixed_size 22880", f".amdhsa_group_segment_fixed_size {lds}")
+        # (the metadata entry of k_emit precedes its .name line)
+        gs = max(i for i in range(nm) if out[i].strip().startswith(".group_segment_fixed_size:"))
+        assert out[gs].strip() == ".group_segment_fixed_size: 22880", out[gs]
+        out[gs] = out[gs].replace("22880", str(lds))
     return out, len(chosen), len(idx)
 
 
-def build(name, spec):
-    out, nsel, n = patched_asm(spec)
+def build(name, spec, vgprs=None, lds=None, init=None):
+    out, nsel, n = patched_asm(spec, vgprs, lds, init)
     d = os.path.join(WORK, name)
     os.makedirs(d, exist_ok=True)
     s = os.path.join(d, "entropy.s")
@@ -154,7 +207,7 @@ def build(name, spec):
     os.makedirs(lib, exist_ok=True)
     run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", os.path.join(lib, "libdmmt_jpeg.so"), *objs,
          "-Wl,-soname,libdmmt_jpeg.so"])
-    print(f"{name}: {nsel} of {n} SDWA instructions of k_emit rewritten -> {lib}")
+    print(f"{name}: {nsel} of {n} SDWA instructions of k_emit rewritten, vgprs {vgprs}, lds {lds}, init {init} -> {lib}")
 
 
 def stage():
@@ -180,7 +233,9 @@ if __name__ == "__main__":
         for j, i in enumerate(sdwa_lines(lines)):
             print(j, i + 1, lines[i].strip())
     elif cmd == "build":
-        build(sys.argv[2], sys.argv[3])
+        opt = [int(x) if x != "-" else None for x in sys.argv[4:6]]
+        opt += [None] * (2 - len(opt))
+        build(sys.argv[2], sys.argv[3], *opt, sys.argv[6] if len(sys.argv) > 6 else None)
     elif cmd == "stage":
         stage()
     else:
