@@ -265,8 +265,8 @@ def test_ppm_error_payload_token_names(L, text, code, token):
 
 
 def test_build_info_reports_no_sdwa_peephole(L):
-    """every device object is built without the SDWA peephole (the round-3/4 study:
-    profiles/r03_kemit_fault_study.md); the library says so"""
+    """every device object is built without the SDWA peephole (no gain with it:
+    profiles/r05_sdwa_ab.txt); the library says so"""
     info = L.dmmt_build_info().decode()
     assert "-amdgpu-sdwa-peephole=false" in info and "gfx950" in info
 
