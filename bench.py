@@ -574,6 +574,9 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
                     help="one process drives all GPUs through the C ABI's multi-GPU context (dmmt_ctx_create_multi)")
     ap.add_argument("--devices", default="",
                     help="--inproc: comma-separated device ids of the members (default 0..gpus-1; repeats allowed)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="N>1 rehearsal on a one-GPU box: every rank on device 0, gloo for the barrier and the "
+                         "gather (RCCL refuses two ranks on one GPU); the line says so (ranks.devices)")
     args = ap.parse_args(argv)
     emit = emit or (lambda line: print(line, flush=True))
     if args.inproc:
@@ -588,12 +591,13 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
     make_encoder = make_encoder or dmmt_jpeg.Encoder
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # the GPU of this rank (--same-device: all on GPU 0, a rehearsal of the N>1 path)
+    local_rank = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a wrong n_gpus")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = "nccl" if torch.cuda.is_available() and not args.same_device else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend=backend)

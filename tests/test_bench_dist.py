@@ -80,6 +80,22 @@ def _worker(rank, world, port, out_dir):
         json.dump({"log": log, "lines": lines}, f)
 
 
+def _worker_same_device(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import bench
+    log, lines = [], []
+
+    def make(lr):
+        log.append(("local_rank", rank, lr))
+        return StandInEncoder(lr, rank, log)
+
+    bench.main(["--gpus", str(world), "--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0",
+                "--config", "1080p420q75x256", "--same-device"], make_encoder=make, emit=lines.append)
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump({"log": log, "lines": lines}, f)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -117,6 +133,20 @@ def test_bench_two_ranks_gloo(tmp_path):
     assert ranks["seconds"][1] > ranks["seconds"][0] * 0.99  # (barrier-bracketed: the slow rank bounds both)
     for sec, rate in zip(ranks["seconds"], ranks["mpixel_s"]):
         assert rate == pytest.approx(w * h * fps * 20 / sec / 1e6, rel=1e-3)
+
+
+@pytest.mark.timeout(300)
+def test_bench_same_device_rehearsal(tmp_path):
+    """--same-device (the N>1 path rehearsed on a one-GPU box): every rank's
+    encoder is created on device 0 and the collectives go over gloo"""
+    world = 2
+    mp.start_processes(_worker_same_device, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    r0 = json.load(open(tmp_path / "rank0.json"))
+    r1 = json.load(open(tmp_path / "rank1.json"))
+    assert [x[2] for x in r0["log"] + r1["log"] if x[0] == "local_rank"] == [0, 0]
+    line = json.loads(r0["lines"][0])
+    assert line["n_gpus"] == 2 and line["config"]["ranks"]["backend"] == "gloo"
 
 
 def test_bench_line_fields_single_rank(monkeypatch):
