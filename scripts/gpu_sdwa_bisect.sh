@@ -4,7 +4,8 @@
 # path and back half, against the oracle (the study tree's determinism script).
 #   bash scripts/gpu_sdwa_bisect.sh [--product] VARIANT...
 # --product also runs tests/test_gpu_parity.py on this tree's SDWA-on build
-# (make VARIANT=sdwa SDWA=1).
+# (make VARIANT=sdwa SDWA=1).  sdwa_study/ is in .gpurunignore: drop that line
+# to run this again.
 set -o pipefail
 O=$PWD/gpurun_out/sdwa_bisect
 S=$PWD/sdwa_study
