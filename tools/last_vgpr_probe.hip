@@ -11,11 +11,16 @@
 #include <stdint.h>
 #include <stdio.h>
 
-enum Op { SHL64_V62, SHL64, SHR64, ASHR64, LSHL_ADD64, MAD_U64_U32, CVT_F64_U32, ADD_U32, MUL_LO_U32, NOPS };
+enum Op {
+    SHL64_V62, SHL64, SHR64, ASHR64, LSHL_ADD64, MAD_U64_U32, CVT_F64_U32, ADD_U32, MUL_LO_U32, SHL32, ALIGNBIT,
+    READLANE, WRITELANE, NOPS
+};
 static const char* kName[NOPS] = {"v_lshlrev_b64, amount in v62 (control)", "v_lshlrev_b64, amount in v63",
                                   "v_lshrrev_b64, amount in v63", "v_ashrrev_i64, amount in v63",
                                   "v_lshl_add_u64, amount in v63", "v_mad_u64_u32, src0 in v63",
-                                  "v_cvt_f64_u32, src in v63", "v_add_u32, src0 in v63", "v_mul_lo_u32, src0 in v63"};
+                                  "v_cvt_f64_u32, src in v63", "v_add_u32, src0 in v63", "v_mul_lo_u32, src0 in v63",
+                                  "v_lshlrev_b32, amount in v63", "v_alignbit_b32, amount in v63",
+                                  "v_readlane_b32 from v63", "v_writelane_b32 into v63"};
 
 struct Sample {
     uint32_t n, a;
@@ -65,12 +70,37 @@ __global__ __launch_bounds__(256) void k_probe(uint32_t* bad, Sample* first, int
                          : "=&v"(r) : "v"(a), "v"((uint32_t)x) : "v63");
             y = r;
             want = (uint32_t)(a + (uint32_t)x);
-        } else {
+        } else if constexpr (OP == MUL_LO_U32) {
             uint32_t r;
             asm volatile("v_mov_b32 v63, %1\n\ts_nop 0\n\tv_mul_lo_u32 %0, v63, %2"
                          : "=&v"(r) : "v"(a | 1u), "v"((uint32_t)x) : "v63");
             y = r;
             want = (uint32_t)((a | 1u) * (uint32_t)x);
+        } else if constexpr (OP == SHL32) {
+            uint32_t r;
+            asm volatile("v_mov_b32 v63, %1\n\ts_nop 0\n\tv_lshlrev_b32 %0, v63, %2"
+                         : "=&v"(r) : "v"(a), "v"((uint32_t)x) : "v63");
+            y = r;
+            want = (uint32_t)x << a;
+        } else if constexpr (OP == ALIGNBIT) {
+            uint32_t r;
+            asm volatile("v_mov_b32 v63, %1\n\ts_nop 0\n\tv_alignbit_b32 %0, %2, %3, v63"
+                         : "=&v"(r) : "v"(a), "v"((uint32_t)(x >> 32)), "v"((uint32_t)x) : "v63");
+            y = r;
+            want = (uint32_t)(x >> a);
+        } else if constexpr (OP == READLANE) {
+            uint32_t r;
+            asm volatile("v_mov_b32 v63, %1\n\ts_nop 4\n\tv_readlane_b32 %0, v63, 5\n\ts_nop 4"
+                         : "=s"(r) : "v"((uint32_t)x) : "v63");
+            y = r;
+            want = (uint32_t)__shfl((int)(uint32_t)x, 5, 64);
+        } else {
+            uint32_t r;
+            const uint32_t sv = __builtin_amdgcn_readfirstlane(a + 100u);
+            asm volatile("v_mov_b32 v63, %1\n\ts_nop 4\n\tv_writelane_b32 v63, %2, 3\n\ts_nop 4\n\tv_mov_b32 %0, v63"
+                         : "=&v"(r) : "v"((uint32_t)x), "s"(sv) : "v63");
+            y = r;
+            want = (threadIdx.x & 63) == 3 ? sv : (uint32_t)x;
         }
         if (y != want) {
             if constexpr (OP == SHL64 || OP == SHR64 || OP == ASHR64) {
@@ -146,6 +176,10 @@ int main() {
         run<CVT_F64_U32>(d, s, blocks, iters);
         run<ADD_U32>(d, s, blocks, iters);
         run<MUL_LO_U32>(d, s, blocks, iters);
+        run<SHL32>(d, s, blocks, iters);
+        run<ALIGNBIT>(d, s, blocks, iters);
+        run<READLANE>(d, s, blocks, iters);
+        run<WRITELANE>(d, s, blocks, iters);
     }
     return 0;
 }
