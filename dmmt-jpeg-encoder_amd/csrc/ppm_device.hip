@@ -465,10 +465,10 @@ __device__ __forceinline__ uint32_t long_token(const PpmText& t, long long ps, b
 struct FastLoads {
     uint4 v[kFastPieces];
     bool full[kFastPieces];
-    uint32_t tw;        // the next chunk's first 16 bytes: a word for each of threads 0-3
-    bool tfull;
-    uint32_t bb;        // the byte before the chunk
-    uint32_t cfirst;    // wave 0: a count of the chunk's row
+    uint32_t pb[kFastPieces];  // lane 0 of a wave: the byte before each of its pieces
+    uint32_t nw[kFastPieces];  // lane 63: the word after each of its pieces
+    bool nfull[kFastPieces];
+    uint32_t cfirst;           // wave 0: a count of the chunk's row
     unsigned long long rbase;
 };
 
@@ -479,29 +479,31 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                                                           long long per, Out* __restrict__ out,
                                                           unsigned long long nsamples, uint32_t maxval) {
     constexpr int NW = kPpmThreads / 64, P = kFastPieces;
-    // the chunk (' ' outside the body) + the next 16 bytes, staged for the
-    // neighbouring pieces' bytes; after the scan the same LDS holds the token
-    // entries in text order (at most one token per two bytes), shifted by the
-    // output's alignment (up to 3 slots) and padded to whole groups of four
-    __shared__ __attribute__((aligned(16))) uint32_t sLds[kFastChunk / 2 + 8];
-    uint32_t* const sText = sLds;
-    uint32_t* const sTok = sLds;
-    static_assert(kFastChunk / 4 + 4 <= kFastChunk / 2, "the staged text fits the entry array");
+    // the token entries in text order (at most one token per two bytes), shifted by
+    // the output's alignment (up to 3 slots) and padded to whole groups of four
+    __shared__ __attribute__((aligned(16))) uint32_t sTok[kFastChunk / 2 + 8];
     __shared__ uint32_t sScan[NW];
     __shared__ unsigned long long sBase;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     // One workgroup per chunk (8 per CU).  Every global load is issued before any
-    // is used: the pieces, the next chunk's first 16 bytes, the byte before the
-    // chunk, and for its first token's index its row's base + the counts before it
-    // in its row.  (Resident workgroups looping over chunks with the next chunk's
-    // loads in flight measured slower: 6 per CU for the registers, 63 vs 49 us.)
+    // is used: the pieces; for a wave's lane 0 the byte before each of its pieces
+    // and for lane 63 the word after each (the neighbours no lane shuffle reaches:
+    // loaded, not staged in LDS -- no barrier before the scan; round 5, 39.9 vs 40.3
+    // us); and for the first token's index the row's base + the counts before the
+    // chunk in its row.  (Resident workgroups looping over chunks with the next
+    // chunk's loads in flight measured slower: 6 per CU for the registers, 63 vs 49 us.)
     auto issue = [&](long long c, FastLoads& f) {
         const long long c0 = c * kFastChunk;
         issue_pieces<P>(t, c0, tid, f.v, f.full);
-        const long long tp = c0 + kFastChunk + 4 * (tid & 3);
-        f.tfull = tp >= t.lo && tp + 4 <= t.len;
-        f.tw = *reinterpret_cast<const uint32_t*>(t.text + (f.tfull ? tp : (t.safe + 15) & ~15ll));
-        f.bb = load_byte_clamped(t, c0 - 1);
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const long long pp = c0 + 16 * (tid + kPpmThreads * q);
+            if (lane == 0) f.pb[q] = load_byte_clamped(t, pp - 1);
+            if (lane == 63) {
+                f.nfull[q] = pp + 16 >= t.lo && pp + 20 <= t.len;
+                f.nw[q] = *reinterpret_cast<const uint32_t*>(t.text + (f.nfull[q] ? pp + 16 : (t.safe + 15) & ~15ll));
+            }
+        }
         const long long row0 = (c / per) * per;
         f.cfirst = counts[min(row0 + lane, c)];
         f.rbase = row_base[c / per];
@@ -516,14 +518,6 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         const long long row0 = (c / per) * per;
         uint32_t w[P][4];
         fix_pieces<P>(t, c0, tid, cur.v, cur.full, w);
-        const uint32_t before = body_sig(t, c0 - 1, cur.bb);
-        uint32_t tw = cur.tw;
-        if (!cur.tfull) {
-            const long long tp = c0 + kFastChunk + 4 * (tid & 3);
-            tw = 0x20202020u;
-            for (int j = 0; j < 4; ++j)
-                if (tp + j >= t.lo && tp + j < t.len) tw = (tw & ~(0xFFu << (8 * j))) | ((uint32_t)t.text[tp + j] << (8 * j));
-        }
         uint32_t cnt = row0 + lane < c ? cur.cfirst : 0u;
         if (wave == 0) {
             for (long long r0 = row0 + 64; r0 < c; r0 += 64) {  // rows of more than 64 chunks (texts > 512 MB)
@@ -532,14 +526,9 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
             }
         }
         const unsigned long long rbase = cur.rbase;
-#pragma unroll
-        for (int q = 0; q < P; ++q)
-            reinterpret_cast<uint4*>(sText)[tid + kPpmThreads * q] = make_uint4(w[q][0], w[q][1], w[q][2], w[q][3]);
-        if (tid < 4) sText[kFastChunk / 4 + tid] = tw;
-        __syncthreads();
-        // token starts per word; a piece's previous byte is the last of piece (q, t - 1):
-        // a lane shuffle, or for a wave's lane 0 the staged byte (the byte before the
-        // chunk for piece 0)
+        // token starts per word; a piece's previous byte is the last of piece (q, t - 1)
+        // and its next word the first of piece (q, t + 1): lane shuffles, loaded for a
+        // wave's lanes 0 and 63 (bytes outside the body read as ' ')
         static_assert(P == 2, "the per-piece counts are scanned as two 16-bit fields");
         uint32_t st[P][4], sg[P][4], wnext[P];
         uint32_t n01 = 0;  // starts per piece, two 16-bit fields
@@ -548,18 +537,20 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         for (int q = 0; q < P; ++q) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) sg[q][k] = sig_bytes(w[q][k]);  // (non-digit token bytes: k_ppm_count)
-            // the neighbouring pieces: the previous one's last byte (lane shuffle; a
-            // wave's lane 0 reads the staged byte, piece 0 the byte before the chunk)
-            // and the next one's first word (lane shuffle; lane 63 reads it staged:
-            // the next wave's lane 0 or, past the chunk, the next chunk's first bytes)
             const int p = tid + kPpmThreads * q;
             uint32_t prev = lane_prev_u32(sg[q][3]);
             wnext[q] = lane_next_u32(w[q][0]);
-            if (lane == 0) {
-                const uint32_t pb = p ? (uint32_t)!ppm_ws((sText[(4 * p - 1)] >> 24)) : before;
-                prev = pb << 31;
+            if (lane == 0) prev = body_sig(t, c0 + 16ll * p - 1, cur.pb[q]) << 31;
+            if (lane == 63) {
+                wnext[q] = cur.nw[q];
+                if (!cur.nfull[q]) {  // past an end of the body
+                    const long long np = c0 + 16ll * (p + 1);
+                    wnext[q] = 0x20202020u;
+                    for (int j = 0; j < 4; ++j)
+                        if (np + j >= t.lo && np + j < t.len)
+                            wnext[q] = (wnext[q] & ~(0xFFu << (8 * j))) | ((uint32_t)t.text[np + j] << (8 * j));
+                }
             }
-            if (lane == 63) wnext[q] = sText[4 * (p + 1)];
             uint32_t nq = 0;
             const uint32_t sgn = sig_bytes(wnext[q]);
 #pragma unroll
@@ -581,7 +572,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
             cnt = wave_sum_full_u32(cnt);
             if (lane == 0) sBase = rbase + cnt;
         }
-        __syncthreads();  // (also: every neighbour read of the staged text is done)
+        __syncthreads();
         uint32_t e01 = i01 - n01, t01 = 0;
 #pragma unroll
         for (int v = 0; v < NW; ++v) {
