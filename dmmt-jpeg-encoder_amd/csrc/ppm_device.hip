@@ -210,11 +210,11 @@ struct PpmText {
 //  k_ppm_count   each chunk's token count: a token starts at every non-whitespace
 //                byte whose previous byte is whitespace (or lies before the body)
 //  k_ppm_rows    one workgroup: exclusive sums of the counts over 1024 rows of chunks
-//  k_ppm_fast    each chunk: the text staged in LDS, its token starts compacted in
-//                text order (a workgroup scan of the per-piece counts), then one
-//                thread per token -- its digits checked and combined with v_dot4
-//                (up to 8 digits; longer tokens are walked) -- and the sample stored
-//                at the chunk's first token index + the token's rank
+//  k_ppm_fast    each chunk: its token starts compacted in text order into LDS
+//                entries (a workgroup scan of the per-piece counts), then one thread
+//                per four tokens -- digits combined with v_dot4 (tokens of four or
+//                more bytes read back and checked, nine or more walked) -- and the
+//                samples stored at the chunk's first token index + the tokens' ranks
 // The pass is optimistic: '#' is not whitespace, so a comment's first byte lies in
 // some token, and that token (like a '+' sign or any other non-digit) fails the
 // digit check and raises `bad`; the host then redoes the body on the general path,
