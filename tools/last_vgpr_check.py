@@ -61,20 +61,12 @@ def code_objects(lib):
 
 
 def vgpr_counts(co_path):
+    """kernel symbol -> .vgpr_count, from the code object's metadata note (one
+    "- .agpr_count: ..." block per kernel, its keys in any order)"""
     notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co_path], capture_output=True, text=True,
                            check=True).stdout
     counts = {}
-    name = None
-    for line in notes.split("\n"):
-        m = re.match(r"\s+\.name:\s+(\S+)", line)
-        if m:
-            name = m.group(1)
-        m = re.match(r"\s+\.vgpr_count:\s+(\d+)", line)
-        if m and name:
-            counts[name] = int(m.group(1))
-    # the kernel's entries list .name after .vgpr_count in some orders: pair by block
-    blocks = re.split(r"\n\s+- \.", notes)
-    for b in blocks:
+    for b in re.split(r"\n\s+- \.", notes):
         n = re.search(r"\.name:\s+(\S+)", b)
         v = re.search(r"\.vgpr_count:\s+(\d+)", b)
         if n and v:
