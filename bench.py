@@ -586,6 +586,9 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
             raise SystemExit("bench: --inproc runs the independent-frame configs")
         return run_inproc(args, emit, make_group or (lambda ids: dmmt_jpeg.Encoder(devices=ids)))
 
+    if args.same_device and args.config in STRIPED:
+        raise SystemExit("bench: --same-device rehearses the independent-frame configs (the stripes' collectives "
+                         "run on GPU tensors)")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # no launcher: start the ranks here
         return spawn_ranks(list(argv if argv is not None else sys.argv[1:]), args.gpus, make_encoder, emit)
     make_encoder = make_encoder or dmmt_jpeg.Encoder
