@@ -10,7 +10,7 @@ per GPU via torch.distributed.run, and `--gpus N` without a launcher spawns the
 N rank processes itself (before anything touches a GPU).
 
 Prints ONE JSON line on rank 0.  `value` comes from the timed region: the
-production path, every call launched directly (six kernels per frame),
+production path, every call launched directly (three kernels per frame),
 consecutive frames pipelined over the context's lanes, the input frames rotating
 over enough distinct slots (> 256 MiB together) that their pixels stream from
 HBM rather than the 256 MiB Infinity Cache.  `roofline` comes from a second
@@ -23,6 +23,12 @@ scripts/kstats_passes.py splits its trace into the two passes (profiles/r03_*).
 `cpu_baseline` times the CPU restatement of the reference encoder (oracle/, C,
 the reference's DCT thread-pool structure) on a bounded sample of the same
 workload on this host.
+`extra_configs` (on by default; `--no-extras` skips it) measures, after the
+headline and on every rank, the BASELINE configs that shard over the GPUs: config
+4 (one 32768x32768 image as MCU-row stripes, with and without restart intervals,
+strong scaling) and config 5 (a stream of 8K 4:2:0 frames at q50/75/95, weak
+scaling), each with its own per-rank block -- so the one `--gpus N` run the
+driver makes per N covers configs 2, 4 and 5.
 """
 import argparse
 import json
@@ -68,7 +74,7 @@ STRIPED = {
 }
 
 
-def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync):
+def run_striped(args, world, rank, local_rank, make_encoder, barrier_sync, xgroup=None):
     """BASELINE config 4: one 32768x32768 image, MCU-row stripes (one per rank).
     "32k420r": a restart interval of one MCU row; per step every rank runs
     dmmt_stripe_analyze, the 544-counter histogram all-reduce, dmmt_stripe_encode
@@ -76,7 +82,9 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
     no restart intervals (the reference's own stream, joined stripes): analyze,
     edge-DC all-gather, histogram all-reduce, measure, (bits, head) all-gather,
     write.  Total work is fixed: scaling "strong"; value = image pixels / MAX
-    elapsed."""
+    elapsed.  The small exchanges run over `xgroup` (bench: a gloo group of CPU
+    tensors, the host reduction of SURVEY.md 8(e); None = the default group).
+    Returns rank 0's line (None on the other ranks)."""
     w, h, sub, quality, rpi = STRIPED[args.config]
     mcu_w, mcu_h = (8, 8) if sub == 0 else ((16, 8) if sub == 1 else (16, 16))
     mcux, mcuy = -(-w // mcu_w), -(-h // mcu_h)
@@ -107,12 +115,12 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
             return enc.stripe_encode(hist, d_out, cap), 0, None
     elif gather:
         def step():
-            n, off, total = dmmt_jpeg.encode_striped(enc, st, opts, d_out, cap)
+            n, off, total = dmmt_jpeg.encode_striped(enc, st, opts, d_out, cap, group=xgroup)
             dmmt_jpeg.gather_striped(out_t, n, off, total, root=0)
             return n, off, total
     else:
         def step():
-            return dmmt_jpeg.encode_striped(enc, st, opts, d_out, cap)
+            return dmmt_jpeg.encode_striped(enc, st, opts, d_out, cap, group=xgroup)
     for _ in range(args.warmup):
         step()
     barrier_sync(enc)
@@ -123,6 +131,7 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
     elapsed = time.perf_counter() - t0
     # (strong scaling: each rank's rate is its stripe's pixels over its own time)
     elapsed, ranks = gather_ranks(elapsed, world, enc, w * (y1 - y0) * args.steps)
+    line = None
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:  # the oracle on a bounded stripe of the same image (256 pixel rows)
@@ -151,6 +160,7 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
                                "no restart intervals (the reference's stream), one MCU-row stripe per GPU joined "
                                "mid-byte, pixels in HBM -> stripe bytes in HBM (edge-DC all-gather, histogram "
                                "all-reduce, bit-count all-gather, size all-gather per step)")
+                            + (f"; exchanges over {dist.get_backend(xgroup)}" if world > 1 else "")
                             + ("; the stripes then sent to one file in rank 0's HBM (gather_striped)" if gather else ""),
                 "width": w, "height": h, "subsampling": ["P444", "P422", "P420"][sub], "quality": quality,
                 "restart_interval": mcux * rpi, "parallelism": f"MCU-row stripes x{world}",
@@ -160,13 +170,89 @@ def run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
             "roofline": None,
             "cpu_baseline": cpu,
         }
-        emit(json.dumps(line))
     enc.free(d_in)
     if not gather:
         enc.free(d_out)
     enc.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return line
+
+
+def run_frame_stream(args, config, world, rank, enc, barrier_sync, steps, warmup):
+    """A stream of independent frames of `config` per rank (BASELINE config 5: 8K
+    4:2:0 at one quality), pipelined over the lanes, every rank its own distinct
+    frames: weak scaling, value = all ranks' pixels / MAX elapsed.  The lean form of
+    the headline measurement (no roofline pass) for extra_configs."""
+    w, h, sub, quality, fps = CONFIGS[config]
+    luma, chroma = dmmt_jpeg.quality_tables(quality)
+    opt_c = dmmt_jpeg.JpegTransformationOptions(dmmt_jpeg.ChromaSubsamplingPreset(sub), 8, luma_table=luma,
+                                                chroma_table=chroma).to_c()
+    frame_bytes = w * h * 3 * fps
+    nslots = max(4, MALL_BYTES // frame_bytes + 2)
+    out_stride = (dmmt_jpeg.max_jpeg_bytes(w, h, sub) + 255) // 256 * 256
+    lanes = max(1, args.lanes)
+    d_in = [enc.malloc(frame_bytes) for _ in range(nslots)]
+    d_out = [enc.malloc(out_stride * fps) for _ in range(lanes)]
+    d_len = [enc.malloc(4 * fps) for _ in range(lanes)]
+    try:
+        for s in range(nslots):
+            enc.fill_synthetic(d_in[s], w, h, fps, first_frame=1000 + (rank * nslots + s) * fps)
+        enc.set_lanes(lanes)
+        for i in range(warmup):
+            enc.encode_device(d_in[i % nslots], fps, w, h, None, d_out[i % lanes], out_stride, d_len[i % lanes],
+                              frame_stride=w * h * 3, opt_c=opt_c)
+        barrier_sync(enc)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            enc.encode_device(d_in[i % nslots], fps, w, h, None, d_out[i % lanes], out_stride, d_len[i % lanes],
+                              frame_stride=w * h * 3, opt_c=opt_c)
+        barrier_sync(enc)
+        elapsed = time.perf_counter() - t0
+        elapsed, ranks = gather_ranks(elapsed, world, enc, w * h * fps * steps)
+        lens = np.frombuffer(enc.d2h(d_len[0], 4 * fps), np.uint32)
+    finally:
+        for p in d_in + d_out + d_len:
+            enc.free(p)
+    if rank != 0:
+        return None
+    return {
+        "metric": f"Mpixel/s encoded ({config})", "value": round(w * h * fps * steps * world / elapsed / 1e6, 2),
+        "unit": "Mpixel/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4), "scaling": "weak",
+        "config": {"workload": f"{w}x{h} synthetic RGB u8, {['4:4:4', '4:2:2', '4:2:0'][sub]}, IJG quality {quality}, "
+                               f"{fps} frame(s) per step per GPU, pixels in HBM -> JPEG files in HBM, {lanes} lanes, "
+                               f"{nslots} input slots",
+                   "quality": quality, "mean_jpeg_bytes": float(lens.mean()), "lanes": lanes, "ranks": ranks},
+    }
+
+
+# the BASELINE configs that shard, measured after the headline (extra_configs):
+# config 4 in both stripe modes (strong scaling), config 5's quality sweep (weak)
+EXTRA_STRIPED = ("32k420r", "32k420")
+EXTRA_STREAM = ("8k420q50", "8k420q75", "8k420q95")
+
+
+def run_extras(args, world, rank, local_rank, make_encoder, enc, barrier_sync, xgroup):
+    """extra_configs: every rank runs each config in turn (the same order on every
+    rank); a config that raises is recorded with its error and the rest still run"""
+    out = {}
+    sargs = argparse.Namespace(**vars(args))
+    sargs.steps, sargs.warmup, sargs.cpu_seconds, sargs.gather = args.extra_steps, 2, 0, False
+    for name in EXTRA_STRIPED:
+        sargs.config = name
+        try:
+            line = run_striped(sargs, world, rank, local_rank, make_encoder, barrier_sync, xgroup)
+        except Exception as e:  # noqa: BLE001 -- reported in the line; the next config still runs
+            line = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            out[name] = line
+    for name in EXTRA_STREAM:
+        try:
+            line = run_frame_stream(args, name, world, rank, enc, barrier_sync, 4 * args.extra_steps, 5)
+        except Exception as e:  # noqa: BLE001
+            line = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            out[name] = line
+    return out
 
 
 def gather_ranks(elapsed, world, enc, pixels_per_rank):
@@ -574,6 +660,13 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
                     help="one process drives all GPUs through the C ABI's multi-GPU context (dmmt_ctx_create_multi)")
     ap.add_argument("--devices", default="",
                     help="--inproc: comma-separated device ids of the members (default 0..gpus-1; repeats allowed)")
+    ap.add_argument("--no-extras", dest="extras", action="store_false",
+                    help="skip extra_configs (BASELINE configs 4 and 5 after the headline)")
+    ap.add_argument("--extra-steps", type=int, default=5,
+                    help="extra_configs: timed steps per striped config (x4 per 8K stream config)")
+    ap.add_argument("--exchange", choices=("host", "device"), default="host",
+                    help="striped configs, N>1: the small exchanges as CPU tensors over gloo (host) or GPU "
+                         "tensors over the main backend (device)")
     ap.add_argument("--same-device", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on device 0, gloo for the barrier and the "
                          "gather (RCCL refuses two ranks on one GPU); the line says so (ranks.devices)")
@@ -586,9 +679,8 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
             raise SystemExit("bench: --inproc runs the independent-frame configs")
         return run_inproc(args, emit, make_group or (lambda ids: dmmt_jpeg.Encoder(devices=ids)))
 
-    if args.same_device and args.config in STRIPED:
-        raise SystemExit("bench: --same-device rehearses the independent-frame configs (the stripes' collectives "
-                         "run on GPU tensors)")
+    if args.same_device and args.config in STRIPED and args.exchange == "device":
+        raise SystemExit("bench: --same-device runs the stripes' exchanges on the host (gloo), not --exchange device")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:  # no launcher: start the ranks here
         return spawn_ranks(list(argv if argv is not None else sys.argv[1:]), args.gpus, make_encoder, emit)
     make_encoder = make_encoder or dmmt_jpeg.Encoder
@@ -613,8 +705,20 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
             torch.cuda.synchronize(dev)
         enc.synchronize()
 
+    # the stripes' small exchanges (histograms, edge DCs, bit counts, sizes): CPU
+    # tensors over gloo, i.e. a host reduction; --exchange device
+    # keeps them on GPU tensors over the main backend (RCCL)
+    xgroup = None
+    if world > 1 and args.exchange == "host" and dist.get_backend() != "gloo":
+        xgroup = dist.new_group(backend="gloo")
+
     if args.config in STRIPED:
-        return run_striped(args, world, rank, local_rank, make_encoder, emit, barrier_sync)
+        line = run_striped(args, world, rank, local_rank, make_encoder, barrier_sync, xgroup)
+        if rank == 0:
+            emit(json.dumps(line))
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     w, h, sub, quality, fps = CONFIGS[args.config]
     luma, chroma = dmmt_jpeg.quality_tables(quality)
@@ -752,9 +856,14 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
             "ppm_to_jpeg": ppm_jpeg,
             "ppm_to_jpeg_stream": ppm_stream,
         }
-        emit(json.dumps(line))
     for p in d_in + d_out + d_len:
         enc.free(p)
+    if args.extras:  # (every rank: the configs' collectives)
+        extras = run_extras(args, world, rank, local_rank, make_encoder, enc, barrier_sync, xgroup)
+        if rank == 0:
+            line["extra_configs"] = extras
+    if rank == 0:
+        emit(json.dumps(line))
     enc.close()
     if world > 1:
         dist.destroy_process_group()

@@ -67,6 +67,35 @@ class StandInEncoder:
     def close(self):
         pass
 
+    # the stripe calls of BASELINE config 4 (extra_configs)
+    def fill_synthetic_rows(self, d, w, h, row0, rows, frame=0):
+        self.log.append(("rows", self.rank, row0, rows))
+
+    stripe = staticmethod(lambda *a, **k: __import__("dmmt_jpeg").Encoder.stripe(*a, **k))
+    stripe_max_bytes = staticmethod(lambda st, opts: 1 << 20)
+
+    def stripe_analyze(self, st, opts):
+        self.log.append(("analyze", self.rank, st.mcu_row0, st.mcu_rows))
+        h = np.zeros(544, np.uint64)
+        h[0] = h[16] = h[272] = h[288] = 7  # a DC and an AC symbol per table
+        return h
+
+    def stripe_encode(self, hist, d_out, cap):
+        self.log.append(("stripe_encode", self.rank, int(np.asarray(hist)[0])))
+        time.sleep(STEP_SLEEP[self.rank])
+        return 1000 + self.rank
+
+    def stripe_dc_edges(self):
+        return [1, 2, 3], [4, 5, 6]
+
+    def stripe_measure(self, hist, prev, d_out, cap):
+        self.log.append(("measure", self.rank, list(prev)))
+        return 8000 + 3 * self.rank, 0xABCD
+
+    def stripe_write(self, bit_offset, next_bits, next16):
+        time.sleep(STEP_SLEEP[self.rank])
+        return 1001
+
 
 def _worker(rank, world, port, out_dir):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
@@ -74,7 +103,7 @@ def _worker(rank, world, port, out_dir):
     import bench
     log, lines = [], []
     bench.main(["--gpus", str(world), "--steps", "20", "--warmup", "2", "--cpu-seconds", "0", "--ppm-steps", "0",
-                "--config", "1080p420q75x256"],
+                "--config", "1080p420q75x256", "--no-extras"],
                make_encoder=lambda lr: StandInEncoder(lr, rank, log), emit=lines.append)
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump({"log": log, "lines": lines}, f)
@@ -91,7 +120,7 @@ def _worker_same_device(rank, world, port, out_dir):
         return StandInEncoder(lr, rank, log)
 
     bench.main(["--gpus", str(world), "--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0",
-                "--config", "1080p420q75x256", "--same-device"], make_encoder=make, emit=lines.append)
+                "--config", "1080p420q75x256", "--same-device", "--no-extras"], make_encoder=make, emit=lines.append)
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump({"log": log, "lines": lines}, f)
 
@@ -157,7 +186,7 @@ def test_bench_line_fields_single_rank(monkeypatch):
         monkeypatch.delenv(k, raising=False)
     import bench
     log, lines = [], []
-    bench.main(["--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0"],
+    bench.main(["--steps", "5", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0", "--no-extras"],
                make_encoder=lambda lr: StandInEncoder(lr, 0, log), emit=lines.append)
     line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["metric"] == "Mpixel/s encoded (4K PPM, q=90)"
@@ -193,7 +222,7 @@ def test_bench_gpus_flag_spawns_ranks(monkeypatch):
     import bench
     lines = []
     bench.main(["--gpus", "2", "--steps", "10", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0",
-                "--config", "1080p420q75x256"], make_encoder=make_standin, emit=lines.append)
+                "--config", "1080p420q75x256", "--no-extras"], make_encoder=make_standin, emit=lines.append)
     assert len(lines) == 1
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "independent frames x2"
@@ -283,3 +312,64 @@ def test_path_roofline_over_the_launched_kernels():
     assert p["valu_frac"] == round(5e6 / 50e-6 / bench.VALU_PEAK_PER_S, 4)
     assert bench.path_roofline(30e6, 500.0, 50e-6, pmc, fused | {"k_offsets"})["valu_frac"] is None
     assert bench.path_roofline(30e6, 500.0, 50e-6, None, fused)["valu_frac"] is None
+
+
+def _worker_extras(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import bench
+    log, lines = [], []
+    bench.main(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--cpu-seconds", "0", "--ppm-steps", "0",
+                "--extra-steps", "2"], make_encoder=lambda lr: StandInEncoder(lr, rank, log), emit=lines.append)
+    with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump({"log": log, "lines": lines}, f)
+
+
+@pytest.mark.timeout(300)
+def test_bench_extra_configs_two_ranks(tmp_path):
+    """`bench.py --gpus 2` (the driver's SCALE command) prints configs 2, 4 and 5 in
+    its one line: after the 4K headline, extra_configs holds BASELINE config 4 (the
+    32768^2 image as one MCU-row stripe per rank, with restart intervals and
+    joined) and config 5 (8K 4:2:0 streams at q50/75/95), each with its own ranks
+    block; the stripes' histograms are summed over the ranks on the host (gloo)"""
+    world = 2
+    mp.start_processes(_worker_extras, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    r0 = json.load(open(tmp_path / "rank0.json"))
+    r1 = json.load(open(tmp_path / "rank1.json"))
+    assert len(r0["lines"]) == 1 and r1["lines"] == []
+    line = json.loads(r0["lines"][0])
+    assert line["metric"] == "Mpixel/s encoded (4K PPM, q=90)" and line["n_gpus"] == 2
+    ex = line["extra_configs"]
+    assert list(ex) == ["32k420r", "32k420", "8k420q50", "8k420q75", "8k420q95"]
+    for name in ("32k420r", "32k420"):
+        e = ex[name]
+        assert "error" not in e, e
+        assert e["scaling"] == "strong" and e["n_gpus"] == 2 and e["steps"] == 2
+        assert e["config"]["ranks"]["world_size"] == 2 and e["config"]["ranks"]["devices"] == [0, 1]
+        assert e["value"] == pytest.approx(32768 * 32768 * 2 / (e["ms_per_step"] * 2 / 1e3) / 1e6, rel=2e-3)
+        assert e["config"]["parallelism"] == "MCU-row stripes x2"
+    # every rank analysed its own half of the 2048 MCU rows, in each stripe mode
+    a0 = {tuple(x[2:]) for x in r0["log"] if x[0] == "analyze"}
+    a1 = {tuple(x[2:]) for x in r1["log"] if x[0] == "analyze"}
+    assert a0 == {(0, 1024)} and a1 == {(1024, 1024)}
+    # the restart-interval stripes encode with the SUM of both ranks' histograms
+    assert {x[2] for x in r0["log"] + r1["log"] if x[0] == "stripe_encode"} == {14}
+    # joined stripes: rank 1's DC predictors continue rank 0's last DCs
+    assert {tuple(x[2]) for x in r1["log"] if x[0] == "measure"} == {(4, 5, 6)}
+    for q in (50, 75, 95):
+        e = ex[f"8k420q{q}"]
+        assert "error" not in e, e
+        assert e["scaling"] == "weak" and e["steps"] == 8 and e["config"]["quality"] == q
+        assert e["config"]["ranks"]["world_size"] == 2
+        assert e["value"] == pytest.approx(7680 * 4320 * 8 * 2 / (e["ms_per_step"] * 8 / 1e3) / 1e6, rel=2e-3)
+
+
+def test_bench_no_extras_by_flag(monkeypatch):
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    import bench
+    lines = []
+    bench.main(["--steps", "2", "--warmup", "0", "--cpu-seconds", "0", "--ppm-steps", "0", "--no-extras"],
+               make_encoder=lambda lr: StandInEncoder(lr, 0, []), emit=lines.append)
+    assert "extra_configs" not in json.loads(lines[0])
