@@ -145,6 +145,18 @@ int hip_err(hipError_t e) {
         if (e_ != hipSuccess) return hip_err(e_); \
     } while (0)
 
+// A fresh allocation lies on the calling thread's current device (every pooled
+// buffer is allocated right after set_device(c)): checked once, here, rather than
+// on every call (a buffer landing on another GPU would still compute correctly over
+// the xGMI mapping, slowly and silently) -- DMMT_E_DEVICE_MISMATCH
+int check_fresh_alloc(void* p) {
+    int cur = -1;
+    HIP_TRY(hipGetDevice(&cur));
+    hipPointerAttribute_t a;
+    HIP_TRY(hipPointerGetAttributes(&a, p));
+    return a.device == cur ? DMMT_OK : DMMT_E_DEVICE_MISMATCH;
+}
+
 // grow a device buffer; zero-fill new memory when `zero`
 int ensure(DevBuf& b, size_t bytes, bool zero = false) {
     if (bytes == 0) bytes = 16;
@@ -153,6 +165,11 @@ int ensure(DevBuf& b, size_t bytes, bool zero = false) {
     b.p = nullptr;
     b.bytes = 0;
     HIP_TRY(hipMalloc(&b.p, bytes));
+    if (int rc = check_fresh_alloc(b.p)) {
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        return rc;
+    }
     b.bytes = bytes;
     if (zero) {
         // on the null stream: finished before any lane (non-blocking streams) runs on it
@@ -403,7 +420,9 @@ int enqueue_encode(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, 
     int rc;
     if ((rc = prepare(c, g, nf, opt, sb, st, &w, lane, async, status))) return rc;
     const int bits = opt->bits_per_channel;
-    if (!c->use_graphs || c->profile)
+    // (a per-file status area -- dmmt_convert_ppm_device_batch -- would put a new
+    // pointer into every file's graph key: that path launches directly)
+    if (!c->use_graphs || c->profile || status)
         return enqueue_direct(c, d_rgb, frame_stride, sb, nf, g, w, bits, out, out_stride, out_len, st);
     std::vector<uint64_t> key = {(uint64_t)(uintptr_t)d_rgb, (uint64_t)frame_stride, (uint64_t)sb, (uint64_t)nf,
                                  (uint64_t)g.width, (uint64_t)g.height, (uint64_t)g.hr, (uint64_t)g.vr,
@@ -543,11 +562,9 @@ extern "C" int dmmt_ctx_create(int device, dmmt_ctx** out) {
     return DMMT_OK;
 }
 
-// The context's device is the calling thread's current one after set_device, and
-// every pooled device buffer it holds (lane workspaces, tables, staging) was
-// allocated on that device -- the multi-GPU readiness check a group's worker runs
-// before a member's work (a member's buffers landing on another GPU would still
-// compute correctly over the xGMI mapping, slowly and silently).
+// Every pooled device buffer the context holds (lane workspaces, tables, staging)
+// lies on the context's device: the on-demand form (dmmt_ctx_check_device) of the
+// check every allocation already passed (check_fresh_alloc).
 static int check_ptr_device(const void* p, int dev) {
     if (!p) return DMMT_OK;
     hipPointerAttribute_t a;
@@ -559,9 +576,6 @@ namespace dmmt {
 int ctx_check_device(dmmt_ctx* c) {
     int rc;
     if ((rc = set_device(c))) return rc;
-    int cur = -1;
-    HIP_TRY(hipGetDevice(&cur));
-    if (cur != c->device) return DMMT_E_DEVICE_MISMATCH;
     std::lock_guard<std::mutex> lk(c->mu);
     for (Lane* L : c->lanes) {
         const DevBuf* bufs[] = {&L->coef,       &L->dcdiff,   &L->lastnz,     &L->ac_hist,    &L->dc_hist,
@@ -1282,7 +1296,7 @@ extern "C" const char* dmmt_strerror(int code) {
     case DMMT_E_OUT_OF_MEMORY: return "Out of device memory";
     case DMMT_E_NO_DEVICE: return "No gfx950 (MI355X) device available; this library has no CPU fallback";
     case DMMT_E_CAPACITY: return "Output buffer too small";
-    case DMMT_E_DEVICE_MISMATCH: return "A member context's thread or buffer is not on its GPU";
+    case DMMT_E_DEVICE_MISMATCH: return "A context's device buffer is not on its GPU";
     default: return dmmt_error_name(code);
     }
 }
@@ -1323,6 +1337,11 @@ extern "C" int dmmt_device_malloc(dmmt_ctx* c, size_t bytes, void** ptr) {
     int rc;
     if ((rc = set_device(c))) return rc;
     HIP_TRY(hipMalloc(ptr, bytes ? bytes : 16));
+    if ((rc = check_fresh_alloc(*ptr))) {
+        (void)hipFree(*ptr);
+        *ptr = nullptr;
+        return rc;
+    }
     return DMMT_OK;
 }
 

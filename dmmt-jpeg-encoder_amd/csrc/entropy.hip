@@ -54,6 +54,9 @@ constexpr int kEmitOcc = kChunkBlocks == 256 ? 7 : 3;  // workgroups per CU
 constexpr int kEmitWords = 4 * kChunkBlocks;
 // Bytes per pass of k_stuffwrite (16 per thread).
 constexpr int kStuffPass = 4096;
+#ifndef DMMT_EMIT_BRANCHFREE
+#define DMMT_EMIT_BRANCHFREE 1  // SlotSink stores a word per piece, no flush branch (0: study builds)
+#endif
 #ifndef DMMT_EMIT_PRIO
 #define DMMT_EMIT_PRIO 1  // k_emit's wave priorities by walk length (0: off, study builds)
 #endif
@@ -143,14 +146,17 @@ __device__ __forceinline__ void zigzag_in_registers(BlockCoef& b) {
 }
 
 // Code tables in LDS as (code, length) pairs: one ds_read_b64 per symbol gives
-// both halves with no masking or shifting.
+// both halves with no masking or shifting.  Every entry is pre-shifted by the
+// category its symbol carries (its low 4 bits; a DC symbol is the category): the
+// code shifted left by cat and the length plus cat, so a piece is the entry ORed
+// with the cat extra bits (ZRL and EOB have category 0).
 template <typename Sink>
 __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const uint2* __restrict__ dctab,
                                            const uint2* __restrict__ actab, Sink& sink, int kmax = 63) {
     {
         const int cat = category_of(dcd);
         const uint2 e = dctab[cat];
-        sink((e.x << cat) | extra_bits(dcd, cat), (int)e.y + cat);
+        sink(e.x | extra_bits(dcd, cat), (int)e.y);
     }
     const uint2 z = actab[0xF0];
     // l16 = 16 * (position of the last non-zero + 1): the zero run before position
@@ -165,7 +171,7 @@ __device__ __forceinline__ void walk_block(const BlockCoef& b, int dcd, const ui
             for (int r = r16 >> 8; r > 0; --r) sink(z.x, (int)z.y);
             const int cat = category_fast(v);
             const uint2 e = actab[(r16 & 0xF0) | cat];
-            sink((e.x << cat) | extra_bits(v, cat), (int)e.y + cat);
+            sink(e.x | extra_bits(v, cat), (int)e.y);
             l16 = 16 * k + 16;
         }
     }
@@ -229,6 +235,21 @@ struct SlotSink {
     unsigned long long acc;
     int nacc;
     int wi;
+#if DMMT_EMIT_BRANCHFREE
+    // Branch-free: the word that holds the top pending bits is stored after every
+    // piece -- complete (and final) when 32 bits are pending, else a partial word at
+    // slot[wi] that a later store or finish() overwrites -- so a piece costs no
+    // exec-mask branch (an s_and_saveexec / s_cbranch / s_or per piece otherwise).
+    __device__ __forceinline__ void operator()(uint32_t val, int len) {
+        acc = (acc << len) | val;
+        nacc += len;               // < 64: at most 31 pending + a piece of at most 32
+        const int full = nacc >> 5;  // 32 bits or more pending: a word is complete
+        nacc &= 31;
+        // past the slot the word lands in its last one: the chunk re-walks then
+        slot[min(wi, kSlotWords - 1) * kEmitThreads] = (uint32_t)(acc >> nacc);
+        wi += full;
+    }
+#else
     __device__ __forceinline__ void operator()(uint32_t val, int len) {
         acc = (acc << len) | val;
         nacc += len;
@@ -239,6 +260,7 @@ struct SlotSink {
             ++wi;
         }
     }
+#endif
     // (the bits after the block in its last word are zero; the slot's later words
     // are stale -- read_slot masks them)
     __device__ __forceinline__ uint32_t finish() {
@@ -318,11 +340,12 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
     const uint32_t tac0 = ct[256 + tt], tac1 = ct[768 + tt];
     const uint32_t tdc = ct[((tt & 31) < 16 ? 0 : 512 - 16) + (tt & 31)];
     const uint32_t lz = lastnz[valid ? e : (long long)frame * g.bpf + el0];
-    if (tid < 256) {
-        sTab[tid] = make_uint2(tac0 & 0xFFFFu, tac0 >> 16);
-        sTab[256 + tid] = make_uint2(tac1 & 0xFFFFu, tac1 >> 16);
+    if (tid < 256) {  // (pre-shifted by the symbol's category, walk_block)
+        const int c = tid & 15;
+        sTab[tid] = make_uint2((tac0 & 0xFFFFu) << c, (tac0 >> 16) + c);
+        sTab[256 + tid] = make_uint2((tac1 & 0xFFFFu) << c, (tac1 >> 16) + c);
     }
-    if (tid < 32) sTab[512 + tid] = make_uint2(tdc & 0xFFFFu, tdc >> 16);
+    if (tid < 32) sTab[512 + tid] = make_uint2((tdc & 0xFFFFu) << (tid & 15), (tdc >> 16) + (tid & 15));
     if (chunk == 0) {  // the histogram replicas k_tables read: zero for the next launch
         for (int i = tid; i < kHistReps * 512; i += kEmitThreads) ac_hist[(size_t)frame * kHistReps * 512 + i] = 0u;
         for (int i = tid; i < kHistReps * 32; i += kEmitThreads) dc_hist[(size_t)frame * kHistReps * 32 + i] = 0u;
@@ -894,6 +917,27 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
             raise_status(status, 16);
         }
         return;
+    }
+    // This chunk's own summary, checked before any store (uniform over the
+    // workgroup, a few scalar compares): its bits fit its staging slot, and its
+    // stuffed bytes -- at most two per scan byte, the closing RST marker included
+    // -- lie between its offset and the next chunk's (the frame total for the last)
+    // inside the frame's output slot.  The summaries come from k_emit and the offsets
+    // scan, so this only fires on a broken producer (the round-5 grouped-offsets
+    // timing ablation, which left the per-chunk offsets unset, stored through them
+    // and faulted: profiles/r05_grouped_offsets_ab.txt); it then raises the capacity
+    // error instead of writing out of bounds.
+    {
+        const unsigned long long cend = last ? tot : cout_next;
+        const unsigned long long sbytes = ((unsigned long long)n + 7) / 8 + 1;
+        if (n > (uint32_t)kChunkWordsCap * 32u || cout > cend || cend > tot ||
+            (unsigned long long)hdr + cout + 2 * sbytes > out_stride) {
+            if (tid == 0) {
+                out_len[frame] = 0;
+                raise_status(status, 16);
+            }
+            return;
+        }
     }
     const ChunkSpan sp = chunk_span(g, c);
     uint8_t* const base = out + (size_t)frame * out_stride + hdr;

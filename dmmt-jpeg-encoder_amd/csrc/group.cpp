@@ -116,9 +116,11 @@ struct Group {
     std::mutex mu;
 };
 
-// A member's readiness on its worker thread, before its part of a call: its GPU is
-// the thread's current device and its pooled buffers (and the group's staging
-// buffers for it) lie there (DMMT_E_DEVICE_MISMATCH otherwise)
+// A member's buffers -- its context's pooled ones and the group's staging buffers
+// for it -- lie on its GPU (DMMT_E_DEVICE_MISMATCH otherwise).  Every allocation is
+// checked when it is made (check_fresh_alloc in encoder.cpp, dmmt_device_malloc), so
+// the calls do not repeat this; dmmt_ctx_check_device runs it on demand, on each
+// member's worker thread.
 static int member_ready(Group* g, int m) {
     int32_t dev = -1;
     int rc = dmmt_ctx_check_device(g->members[m], &dev);
@@ -190,7 +192,6 @@ int group_encode_batch(Group* g, const dmmt_image* imgs, int n, const dmmt_optio
             idx.push_back(k);
         }
         if (sub.empty()) return;
-        if ((rcs[m] = member_ready(g, m))) return;
         std::vector<uint8_t*> o(sub.size(), nullptr);
         std::vector<size_t> l(sub.size(), 0);
         rcs[m] = dmmt_jpeg_encode_batch(g->members[m], sub.data(), (int)sub.size(), opt, o.data(), l.data());
@@ -234,7 +235,6 @@ int run_stripes(Workers* w, const std::vector<dmmt_ctx*>& ctxs, const std::vecto
     std::vector<std::vector<uint64_t>> hist(S, std::vector<uint64_t>(DMMT_STRIPE_HIST_WORDS, 0));
     std::vector<int16_t> first(3 * S, 0), last(3 * S, 0);
     par([&](int k) {
-        if ((rcs[k] = dmmt_ctx_check_device(ctxs[k], nullptr))) return;  // (its worker: the readiness check)
         if ((rcs[k] = prep(k))) return;
         if ((rcs[k] = dmmt_stripe_analyze(ctxs[k], &st[k], opt, hist[k].data()))) return;
         if (joined) rcs[k] = dmmt_stripe_dc_edges(ctxs[k], &first[3 * k], &last[3 * k]);
@@ -359,7 +359,7 @@ int group_encode_striped(Group* g, const dmmt_image* img, const dmmt_options* op
         if ((rc = grow(ctxs[k], &b.out, &b.out_cap, cap))) return rc;
         d_outs[k] = (uint8_t*)b.out;
         caps[k] = b.out_cap;
-        return member_ready(g, k);
+        return (int)DMMT_OK;
     };
     std::vector<uint64_t> lens;
     int rc = run_stripes(g->workers, ctxs, st, opt, d_outs, caps, lens, prep);

@@ -57,7 +57,7 @@ enum dmmt_status {
     DMMT_E_OUT_OF_MEMORY = -201,
     DMMT_E_NO_DEVICE = -202,                /* no gfx950 device visible: there is no CPU fallback */
     DMMT_E_CAPACITY = -203,                 /* caller-provided device output buffer too small */
-    DMMT_E_DEVICE_MISMATCH = -204           /* a context's thread or pooled buffer is not on its GPU */
+    DMMT_E_DEVICE_MISMATCH = -204           /* a context's pooled buffer is not on its GPU */
 };
 
 /* ChromaSubsamplingPreset (subsampling.rs:11-55) */
@@ -337,12 +337,12 @@ int dmmt_ctx_set_profiling(dmmt_ctx* ctx, int enable);
 int dmmt_ctx_profile(dmmt_ctx* ctx, double* ms, int32_t* launches, int n_stages);
 int dmmt_num_stages(void);
 const char* dmmt_stage_name(int stage);
-/* Multi-GPU readiness: the context's GPU is the current device of the thread that works for
- * it, and every pooled device buffer of the context lies on that GPU (hipPointerGetAttributes);
- * for a multi-GPU context every member is checked on its own host thread, with the group's
- * pooled staging buffers.  The group workers run the same check before each member's part
- * of a call.  *device (may be NULL): the context's (first) device.  DMMT_E_DEVICE_MISMATCH
- * on a mismatch. */
+/* Multi-GPU readiness: every pooled device buffer of the context lies on the context's GPU
+ * (hipPointerGetAttributes); for a multi-GPU context every member is checked on its own
+ * host thread, with the group's pooled staging buffers.  Every allocation the library makes
+ * (pooled buffers, dmmt_device_malloc) is checked once, when it is made, against the
+ * device the context bound the thread to; the calls do not repeat the check.  *device (may
+ * be NULL): the context's (first) device.  DMMT_E_DEVICE_MISMATCH on a mismatch. */
 int dmmt_ctx_check_device(dmmt_ctx* ctx, int32_t* device);
 /* device memory for callers without their own allocator (bench, tests) */
 int dmmt_device_malloc(dmmt_ctx* ctx, size_t bytes, void** ptr);

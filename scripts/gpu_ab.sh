@@ -11,7 +11,7 @@ for spec in $2; do
   v=${spec%%:*}; envs=""; [ "$spec" != "$v" ] && envs=${spec#*:}
   if [ "$v" = base ]; then unset DMMT_LIB_PATH; else export DMMT_LIB_PATH=$PWD/dmmt-jpeg-encoder_amd/lib_$v/libdmmt_jpeg.so; fi
   tag=$(echo "$spec" | tr ':,=' '___')
-  env ${envs//,/ } timeout -k 10 200 python bench.py --config $c --steps ${STEPS:-200} --warmup ${WARMUP:-20} --cpu-seconds 0 --ppm-steps 0 > gpurun_out/ab/$c.$tag.json 2> gpurun_out/ab/$c.$tag.err || { echo "spec $spec failed"; tail -3 gpurun_out/ab/$c.$tag.err; exit 1; }
+  env ${envs//,/ } timeout -k 10 200 python bench.py --config $c --steps ${STEPS:-200} --warmup ${WARMUP:-20} --cpu-seconds 0 --ppm-steps 0 --no-extras > gpurun_out/ab/$c.$tag.json 2> gpurun_out/ab/$c.$tag.err || { echo "spec $spec failed"; tail -3 gpurun_out/ab/$c.$tag.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/ab/$c.$tag.json')); k=d['roofline']['kernels']; print('$c', '$spec', d['value'], d['ms_per_step'], d['config']['single_lane_ms_per_step'], ' '.join(f'{n[2:]}={v[\"avg_launch_us\"]}' for n, v in k.items()))"
 done
 done

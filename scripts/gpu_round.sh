@@ -15,7 +15,7 @@ timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --
 tail -1 $O/gpu_tests.log
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail $O/bench.err; exit 1; }
 cat $O/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py > $O/bench_prof.json 2> $O/bench_prof.err || { echo "rocprof bench failed"; tail $O/bench_prof.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-extras > $O/bench_prof.json 2> $O/bench_prof.err || { echo "rocprof bench failed"; tail $O/bench_prof.err; exit 1; }
 f=$(find $O/prof -name 'run_kernel_stats.csv' | head -1)
 cp $f $O/kernel_stats.csv
 python scripts/kstats.py $f

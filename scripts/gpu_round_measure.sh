@@ -7,7 +7,7 @@ O=gpurun_out/measure/$TAG
 mkdir -p $O
 run() {  # name, args...
   local n=$1; shift
-  timeout -k 10 300 python bench.py --cpu-seconds 0 "$@" > $O/$n.json 2> $O/$n.err || { echo "bench $n failed"; tail $O/$n.err; exit 1; }
+  timeout -k 10 300 python bench.py --cpu-seconds 0 --no-extras "$@" > $O/$n.json 2> $O/$n.err || { echo "bench $n failed"; tail $O/$n.err; exit 1; }
   python -c "import json,sys; d=json.load(open('$O/$n.json')); print('$n', d['value'], d['ms_per_step'], d['steps'])"
 }
 run 4k444q90 --steps 400 --warmup 40

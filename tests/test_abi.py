@@ -310,3 +310,14 @@ def test_last_vgpr_check_flags_the_probe(tmp_path):
     flagged = {ins.split()[0] for _, cnt, last, ins in hits if last == 63 and cnt == 64}
     assert {"v_lshlrev_b64", "v_lshrrev_b64", "v_ashrrev_i64"} <= flagged
     assert not any("v62" in ins for _, _, _, ins in hits)
+    # the same probe as a compressed offload bundle (--offload-compress): unpacked with
+    # clang-offload-bundler, the same hits
+    clib = tmp_path / "libprobe_c.so"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "--offload-compress", "-shared", "-fPIC",
+                    "-o", str(clib), os.path.join(ROOT, "tools", "last_vgpr_probe.hip")], check=True,
+                   capture_output=True)
+    assert chk.elf_section(str(clib), ".hip_fatbin")[:4] == b"CCOB"
+    chits = []
+    for co in chk.code_objects(str(clib)):
+        chits += chk.check_object(co)[0]
+    assert sorted(chits) == sorted(hits)

@@ -143,8 +143,10 @@ def test_bench_two_ranks_gloo(tmp_path):
     # distinct synthetic frames per rank (no two ranks encode the same frames)
     f0 = {tuple(x[2:]) for x in r0["log"] if x[0] == "frames"}
     f1 = {tuple(x[2:]) for x in r1["log"] if x[0] == "frames"}
-    # the timed steps run pipelined over the default lanes, then one at a time with events (roofline)
-    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 1]
+    # untimed settle steps, then the timed steps, pipelined over the default lanes, then one at a
+    # time with events (roofline)
+    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 4, 1]
+    assert line["config"]["settle"]["frames"] >= 32 * 256 and line["config"]["settle"]["ms"] >= 60
     assert line["config"]["lanes"] == 4 and line["config"]["single_lane_ms_per_step"] > 0
     assert f0 and f1 and not (f0 & f1)
     # elapsed is the MAX over ranks: at least the slow rank's sleeps
