@@ -19,5 +19,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 f=$(find $O/prof -name 'run_kernel_stats.csv' | head -1)
 cp $f $O/kernel_stats.csv
 python scripts/kstats.py $f
-python scripts/kstats_passes.py $(dirname $f)/run_kernel_trace.csv $O/kernel_passes.csv
+python scripts/kstats_passes.py $(dirname $f)/run_kernel_trace.csv $O/kernel_passes.csv 20 200 $O/bench_prof.json
 echo exit=0

@@ -1,12 +1,13 @@
 """Per-kernel rocprofv3 durations of bench.py split into its passes.
 
-bench.py (default arguments) dispatches every k_* kernel W + K times in the
-pipelined timed pass, then W + K times in the roofline pass (one frame at a
+bench.py (default arguments) dispatches every k_* kernel S times in the untimed
+settle phase (config.settle.frames of its line), W + K times in the pipelined timed
+pass, then W + K times in the roofline pass (one frame at a
 time, HIP events around each launch).  rocprofv3 --stats averages all of them;
 this splits run_kernel_trace.csv by dispatch order so the roofline pass's
 average can be compared with the `roofline.kernels[*].avg_launch_us` the bench
 line reports for the same dispatches.
-usage: kstats_passes.py <run_kernel_trace.csv> <out.csv> [warmup steps]
+usage: kstats_passes.py <run_kernel_trace.csv> <out.csv> [W] [K] [S | bench line .json]
 """
 import csv
 import sys
@@ -15,6 +16,14 @@ from collections import defaultdict
 trace, out = sys.argv[1], sys.argv[2]
 W = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 K = int(sys.argv[4]) if len(sys.argv) > 4 else 200
+S = 0
+if len(sys.argv) > 5:
+    a = sys.argv[5]
+    if a.endswith(".json"):  # the bench line of the same run: its settle frame count
+        import json
+        S = int((json.load(open(a))["config"].get("settle") or {}).get("frames", 0))
+    else:
+        S = int(a)
 per = defaultdict(list)
 for r in sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Dispatch_Id"])):
     name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dmmt::", "").split("<")[0]
@@ -23,7 +32,7 @@ for r in sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Dispatch_Id"])
 rows = []
 for name, d in per.items():
     n = W + K
-    passes = {"timed_pipelined": d[:n], "roofline_one_lane": d[n:2 * n], "all": d}
+    passes = {"settle": d[:S], "timed_pipelined": d[S:S + n], "roofline_one_lane": d[S + n:S + 2 * n], "all": d}
     for p, v in passes.items():
         if v:
             rows.append({"kernel": name, "pass": p, "dispatches": len(v), "avg_us": round(sum(v) / len(v), 2),
