@@ -10,8 +10,10 @@ per GPU via torch.distributed.run, and `--gpus N` without a launcher spawns the
 N rank processes itself (before anything touches a GPU).
 
 Prints ONE JSON line on rank 0.  `value` comes from the timed region: the
-production path, every call launched directly (three kernels per frame),
-consecutive frames pipelined over the context's lanes, the input frames rotating
+production path, every call launched directly (four kernels per frame: k_front,
+k_hist with the fused tables, k_emit with the fused offsets, k_stuffwrite),
+consecutive frames pipelined over the context's lanes, after an untimed settle
+phase of the same steps (--settle-ms, profiles/r06_settle_study.txt), the input frames rotating
 over enough distinct slots (> 256 MiB together) that their pixels stream from
 HBM rather than the 256 MiB Infinity Cache.  `roofline` comes from a second
 pass over the same steps, one frame at a time, with HIP events around every
@@ -19,7 +21,8 @@ kernel launch, recorded on the stream the kernel runs on: per kernel the average
 launch duration, the SURVEY.md 8(d) algorithmic bytes over it, and the PMC
 traffic from profiles/; the dominant (longest) kernel is the headline.
 `rocprofv3 --kernel-trace` of this command times the same dispatches:
-scripts/kstats_passes.py splits its trace into the two passes (profiles/r03_*).
+scripts/kstats_passes.py splits its trace into the settle phase and the two
+passes (profiles/r06_v01_kernel_passes.csv).
 `cpu_baseline` times the CPU restatement of the reference encoder (oracle/, C,
 the reference's DCT thread-pool structure) on a bounded sample of the same
 workload on this host.

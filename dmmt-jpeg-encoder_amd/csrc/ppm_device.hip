@@ -48,7 +48,7 @@ constexpr int kPpmCarryThreads = 1024;
 // takes kCountChunks chunks per workgroup (4 pieces per thread)
 constexpr int kFastPieces = 2;
 constexpr int kFastChunk = 16 * kFastPieces * kPpmThreads;
-constexpr int kCountChunks = 2;  // (1 and 4 measured slower)
+constexpr int kCountChunks = 2;  // (1 and 4 measured slower, profiles/STUDIES.md F)
 
 // Transition maps: entry state s = (in comment) << 1 | (last kept byte a token
 // byte); entry s occupies bits [16s, 16s + 16): exit state << 14 | tokens started.

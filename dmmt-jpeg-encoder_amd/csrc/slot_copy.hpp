@@ -23,7 +23,7 @@
 // past the block's words when sh > 0 and the block's tail is shorter than sh.
 // Unmasked, those stale bits land right behind the block's last bit -- exactly
 // where the next block's copy_head ORs its head -- as extra 1 bits.  That was the
-// round-4 one-bit parity failure of the first clear-free build.
+// round-4 one-bit parity failure of the first clear-free build (profiles/STUDIES.md B).
 #pragma once
 #include <stdint.h>
 

@@ -5,7 +5,7 @@ chunk's stream [binary_stream.rs:38-66].
 The unmasked replay is the first clear-free build of round 4 (stale slot words
 past a block not zeroed): the check must find its fault, and the fault must be
 extra 1 bits only -- the symptom of the round-4 `r04_emit1` parity failure
-(8K 4:2:0 q95, b'\\x16' -> b'\\x1e')."""
+(8K 4:2:0 q95, b'\\x16' -> b'\\x1e'; profiles/STUDIES.md B)."""
 import os
 import shutil
 import subprocess
