@@ -71,7 +71,7 @@ struct Lane {
     int* status = nullptr;   // [2][kStatusWords], host-mapped
     int* dstatus = nullptr;  // its device address
     DevBuf coef, dcdiff, lastnz, ac_hist, dc_hist, code_tab, hdr_len, total_out, stage, chunk_bits, chunk_ff,
-        chunk_edge, chunk_bit0, chunk_out, arrive;
+        chunk_ff8, chunk_edge, chunk_bit0, chunk_out, arrive;
     // dmmt_convert_ppm_device_batch: a file's samples and its comment-free decode state
     DevBuf ppm_rgb, ppm_counts, ppm_rowbase;
 };
@@ -259,6 +259,8 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     if ((rc = ensure(L->stage, (nch * (size_t)kChunkWordsCap + 64) * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(L->chunk_bits, nch * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(L->chunk_ff, nch * 8 * sizeof(uint32_t)))) return rc;
+    // (k_emit's fused offsets read the packed counts 16 bytes at a time: two past the end)
+    if ((rc = ensure(L->chunk_ff8, (nch + 2) * sizeof(unsigned long long)))) return rc;
     if ((rc = ensure(L->chunk_edge, nch * sizeof(uint32_t)))) return rc;
     if ((rc = ensure(L->chunk_bit0, nch * sizeof(unsigned long long)))) return rc;
     if ((rc = ensure(L->chunk_out, nch * sizeof(unsigned long long)))) return rc;
@@ -292,6 +294,7 @@ int ensure_work(dmmt_ctx* c, const Geom& g, int nf, Work* w, int lane, bool asyn
     w->stage = (uint32_t*)L->stage.p;
     w->chunk_bits = (uint32_t*)L->chunk_bits.p;
     w->chunk_ff = (uint32_t*)L->chunk_ff.p;
+    w->chunk_ff8 = (unsigned long long*)L->chunk_ff8.p;
     w->chunk_edge = (uint32_t*)L->chunk_edge.p;
     w->chunk_bit0 = (unsigned long long*)L->chunk_bit0.p;
     w->chunk_out = (unsigned long long*)L->chunk_out.p;
@@ -515,8 +518,8 @@ void destroy_lane(Lane* L, bool own_stream) {
     if (L->status) (void)hipHostFree(L->status);
     DevBuf* bufs[] = {&L->coef,      &L->dcdiff,     &L->lastnz,     &L->ac_hist,
                       &L->dc_hist,  &L->code_tab,  &L->hdr_len,    &L->total_out,  &L->stage,
-                      &L->chunk_bits, &L->chunk_ff, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out, &L->arrive,
-                      &L->ppm_rgb,    &L->ppm_counts, &L->ppm_rowbase};
+                      &L->chunk_bits, &L->chunk_ff, &L->chunk_ff8, &L->chunk_edge, &L->chunk_bit0, &L->chunk_out,
+                      &L->arrive,     &L->ppm_rgb,    &L->ppm_counts, &L->ppm_rowbase};
     for (DevBuf* b : bufs) release(*b);
     if (own_stream) (void)hipStreamDestroy(L->stream);
     delete L;
@@ -580,7 +583,7 @@ int ctx_check_device(dmmt_ctx* c) {
     for (Lane* L : c->lanes) {
         const DevBuf* bufs[] = {&L->coef,       &L->dcdiff,   &L->lastnz,     &L->ac_hist,    &L->dc_hist,
                                 &L->code_tab,   &L->hdr_len,  &L->total_out,  &L->stage,      &L->chunk_bits,
-                                &L->chunk_ff,   &L->chunk_edge, &L->chunk_bit0, &L->chunk_out, &L->arrive,
+                                &L->chunk_ff,   &L->chunk_ff8,  &L->chunk_edge, &L->chunk_bit0, &L->chunk_out, &L->arrive,
                                 &L->ppm_rgb,    &L->ppm_counts, &L->ppm_rowbase};
         for (const DevBuf* b : bufs)
             if ((rc = check_ptr_device(b->p, c->device))) return rc;

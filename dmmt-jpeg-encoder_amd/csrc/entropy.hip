@@ -57,6 +57,9 @@ constexpr int kStuffPass = 4096;
 #ifndef DMMT_EMIT_BRANCHFREE
 #define DMMT_EMIT_BRANCHFREE 1  // SlotSink stores a word per piece, no flush branch (0: study builds)
 #endif
+#ifndef DMMT_TAIL_DMA
+#define DMMT_TAIL_DMA 1  // fused offsets: the packed 0xFF counts land in LDS with the first loads (0: study builds)
+#endif
 #ifndef DMMT_EMIT_PRIO
 #define DMMT_EMIT_PRIO 1  // k_emit's wave priorities by walk length (0: off, study builds)
 #endif
@@ -279,10 +282,16 @@ __device__ __forceinline__ uint32_t bits16_at(uint32_t a, uint32_t b, int p) {
     return (uint32_t)(x >> (48 - (p & 31))) & 0xFFFFu;
 }
 
+struct NoMark {
+    template <typename I>
+    __device__ void operator()(I) const {}
+};
+template <typename Mark = NoMark>
 __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ cff,
+                              const unsigned long long* __restrict__ cff8, uint8_t* sFF8,
                               const uint32_t* __restrict__ cedge, const Geom& g, unsigned long long* __restrict__ bit0,
                               unsigned long long* __restrict__ outo, unsigned long long* __restrict__ total,
-                              unsigned long long* sWaveV, int* sWaveF);
+                              unsigned long long* sWaveV, int* sWaveF, Mark mark = Mark());
 static_assert(kArriveWords == kArriveFrameWords, "the host sizes the counters");
 
 // ---------------------------------------------------------------------- k_emit
@@ -298,14 +307,15 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
                                               int fuse, uint32_t* __restrict__ arrive,
                                               unsigned long long* __restrict__ chunk_bit0,
                                               unsigned long long* __restrict__ chunk_out,
-                                              unsigned long long* __restrict__ total_out) {
+                                              unsigned long long* __restrict__ total_out,
+                                              unsigned long long* __restrict__ chunk_ff8) {
     // code tables: [luma AC 256][chroma AC 256][luma DC 16][chroma DC 16]
     __shared__ uint2 sTab[2 * 256 + 2 * 16];
     // the window image; during the sort and the walk its first words hold the
     // walk order, the keys and the blocks' bit counts (read before the window
     // loop, whose first clear follows two barriers)
     __shared__ uint32_t sW[kEmitWords + 2];
-    __shared__ uint32_t sSlot[kSlotWords * kEmitThreads];
+    __shared__ __attribute__((aligned(16))) uint32_t sSlot[kSlotWords * kEmitThreads];
     __shared__ uint32_t sWave[kEmitWaves];
     __shared__ uint32_t sFF[8];
     __shared__ uint32_t sEdge[3];  // word 0, the two words holding bits total-16 .. total-1
@@ -505,20 +515,31 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
             last16 = bits16_at(sEdge[1], sEdge[2], (int)(total - 16));
         else
             last16 = total ? sEdge[0] >> (32 - total) : 0u;
+        unsigned long long f8 = 0;  // the same counts one byte each (fused_offsets reads them with its first loads)
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
+        for (int r = 0; r < 8; ++r) {
             __hip_atomic_store(chunk_ff + cid * 8 + r, sFF[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            f8 |= (unsigned long long)min(sFF[r], 255u) << (8 * r);
+        }
+        __hip_atomic_store(chunk_ff8 + cid, f8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(chunk_bits + cid, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(chunk_edge + cid, (first16 << 16) | last16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (fuse) {  // (uniform) count this workgroup in once its summary is published (arrive_last)
         if (tid == 0) sLast = arrive_last(arrive + (size_t)frame * kArriveWords, chunk, (unsigned)g.nch);
         __syncthreads();
+        DMMT_TRACE(6);
         if (sLast) {  // every other chunk of the frame is done: its offsets
             arrive_acquire();
             const size_t fb = (size_t)frame * g.nch;
-            fused_offsets(chunk_bits + fb, chunk_ff + fb * 8, chunk_edge + fb, g, chunk_bit0 + fb, chunk_out + fb,
-                          total_out + frame, sOffV, sOffF);
+#ifdef DMMT_PHASE_TRACE
+            auto mark = [&](auto i) { DMMT_TRACE(decltype(i)::value); };
+#else
+            NoMark mark;
+#endif
+            // (the packed counts go to sSlot, which no wave reads any more)
+            fused_offsets(chunk_bits + fb, chunk_ff + fb * 8, chunk_ff8 + fb, reinterpret_cast<uint8_t*>(sSlot),
+                          chunk_edge + fb, g, chunk_bit0 + fb, chunk_out + fb, total_out + frame, sOffV, sOffF, mark);
         }
     }
     DMMT_TRACE(3);
@@ -652,12 +673,17 @@ __device__ __forceinline__ unsigned long long block_segscan_1024(bool f, unsigne
 // bit scan comes first, then only the 0xFF count at each chunk's own alignment
 // residue is loaded.  sWaveV holds kEmitWaves + 1 words (the last: the carry).
 static_assert(kFusedRoundChunks % kEmitThreads == 0, "whole chunks per thread of the fused offsets");
+static_assert(kFusedRoundChunks % (2 * kEmitThreads) == 0 && kFusedRoundChunks * 8 <= kSlotWords * kEmitThreads * 4,
+              "a round's packed 0xFF counts: whole 16-byte pieces per thread, inside k_emit's slot area");
 static_assert((unsigned long long)kFusedOffsetsMaxChunks * kChunkBlocks * kMaxBlockBits < (1ull << 32),
               "a fused frame's bit offsets fit 32 bits");
+// (mark: phase marks of the tracer build, DMMT_PHASE_TRACE; a no-op otherwise)
+template <typename Mark>
 __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits, const uint32_t* __restrict__ cff,
+                              const unsigned long long* __restrict__ cff8, uint8_t* sFF8,
                               const uint32_t* __restrict__ cedge, const Geom& g, unsigned long long* __restrict__ bit0,
                               unsigned long long* __restrict__ outo, unsigned long long* __restrict__ total,
-                              unsigned long long* sWaveV, int* sWaveF) {
+                              unsigned long long* sWaveV, int* sWaveF, Mark mark) {
     // (32-bit offsets: the static_assert above; they keep the chunks' state in few registers)
     constexpr int KP = kFusedRoundChunks / kEmitThreads, NT = kEmitThreads;
     const int tid = threadIdx.x;
@@ -667,6 +693,21 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
         const int rn = min(kFusedRoundChunks, nch - r0);
         const int per = (rn + NT - 1) / NT;  // <= KP
         const int c0 = r0 + min(tid * per, rn), c1 = r0 + min(tid * per + per, rn);
+#if DMMT_TAIL_DMA
+        // The round's packed 0xFF counts straight into LDS (global_load_lds, 16 bytes =
+        // two chunks per lane, sc1: agent scope like ld_agent), issued with the loads
+        // below: the count at each chunk's residue is then an LDS read, not a second
+        // round trip.  The first barrier of the bit scan waits for them.
+        {
+            const int npairs = (rn + 1) >> 1;
+#pragma unroll
+            for (int i = 0; i < kFusedRoundChunks / 2 / NT; ++i) {
+                const int pc = min(i * NT + tid, npairs - 1);  // (a chunk past an odd round's end: the padding)
+                __builtin_amdgcn_global_load_lds((const void*)(cff8 + r0 + 2 * pc),
+                                                 (void*)(sFF8 + 16 * (i * NT + (tid & ~63))), 16, 0, 16);
+            }
+        }
+#endif
         uint32_t nbits[KP], edge[KP];
 #pragma unroll
         for (int i = 0; i < KP; ++i) {  // every load issued before any is used (clamped indices)
@@ -695,6 +736,7 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
             if (c0 + i < c1) seg_combine(f, v, (firstm >> i) & 1u, nbits[i] + (c0 + i == 0 ? (uint32_t)g.bit_phase : 0u));
         bool fx;
         const uint32_t ex = (uint32_t)block_segscan_nw<kEmitWaves>(f, v, sWaveV, sWaveF, &fx);
+        mark(std::integral_constant<int, 7>{});  // the bits and edges loaded, the bit scan
         uint32_t run = fx ? ex : carry_run + ex;  // (a segment start before it in this round resets the carry)
         uint32_t b0[KP];
 #pragma unroll
@@ -708,9 +750,19 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
         }
         if (c0 < c1 && c1 == r0 + rn) sWaveV[kEmitWaves] = run;  // the round's last chunk: the next carry
         uint32_t ob[KP];
+#if DMMT_TAIL_DMA
+#pragma unroll
+        for (int i = 0; i < KP; ++i) {  // the 0xFF bytes inside the chunk at its actual alignment
+            const int cc = min(c0 + i, nch - 1);
+            const uint32_t slot = (8u - (b0[i] & 7u)) & 7u;
+            ob[i] = sFF8[8 * (cc - r0) + slot];
+            if (ob[i] == 255u) ob[i] = ld_agent(cff + (size_t)cc * 8 + slot);  // a count the byte cannot hold
+        }
+#else
 #pragma unroll
         for (int i = 0; i < KP; ++i)  // the 0xFF bytes inside the chunk at its actual alignment
             ob[i] = ld_agent(cff + (size_t)min(c0 + i, nch - 1) * 8 + ((8 - (b0[i] & 7)) & 7));
+#endif
         uint32_t mine = 0;
 #pragma unroll
         for (int i = 0; i < KP; ++i) {
@@ -735,8 +787,10 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
             ob[i] = o;
             mine += o;
         }
+        mark(std::integral_constant<int, 8>{});  // the 0xFF counts at each chunk's residue loaded, the bytes
         unsigned long long tot = 0;
         uint32_t orun = carry_out + (uint32_t)block_scan_nw<kEmitWaves>(mine, sWaveV, &tot);  // (its barriers publish the carry)
+        mark(std::integral_constant<int, 9>{});  // the byte scan
 #pragma unroll
         for (int i = 0; i < KP; ++i) {
             const int c = c0 + i;
@@ -748,6 +802,7 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
         carry_out += (uint32_t)tot;
         carry_run = (uint32_t)sWaveV[kEmitWaves];
         __syncthreads();  // (the carry word is rewritten by the next round)
+        mark(std::integral_constant<int, 10>{});  // the offsets stored
     }
     if (tid == 0) *total = carry_out;
 }
@@ -1044,7 +1099,8 @@ hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_off
     const int fuse = fuse_offsets && offsets_fusable(g) ? 1 : 0;
     hipLaunchKernelGGL(k_emit, dim3(g.nch, n_frames), dim3(kEmitThreads), 0, st, (const int16_t*)w.coef,
                        (const int16_t*)w.dcdiff, (const uint8_t*)w.lastnz, (const uint32_t*)w.code_tab, g, w.stage, w.chunk_bits, w.chunk_ff,
-                       w.chunk_edge, w.ac_hist, w.dc_hist, fuse, w.arrive, w.chunk_bit0, w.chunk_out, w.total_out);
+                       w.chunk_edge, w.ac_hist, w.dc_hist, fuse, w.arrive, w.chunk_bit0, w.chunk_out, w.total_out,
+                       w.chunk_ff8);
     return hipGetLastError();
 }
 

@@ -19,6 +19,7 @@ struct Work {
     uint32_t* stage;                // [frames][nch][kChunkWordsCap] each chunk's own bit stream, MSB first
     uint32_t* chunk_bits;           // [frames][nch] bits of the chunk
     uint32_t* chunk_ff;             // [frames][nch][8] 0xFF bytes inside the chunk per alignment residue
+    unsigned long long* chunk_ff8;  // [frames * nch + 2] the same eight counts one byte each (255: take chunk_ff's)
     uint32_t* chunk_edge;           // [frames][nch] first 16 bits << 16 | last 16 bits
     unsigned long long* chunk_bit0; // [frames][nch] bit offset of the chunk in its restart segment
     unsigned long long* chunk_out;  // [frames][nch] offset of the chunk's output bytes after the header

@@ -23,7 +23,9 @@ NAMES = {
                 4: "front E symbols", 5: "front hist flush", 10: "tables 1 hist", 6: "tables merge leafsearch", 7: "tables merge pkgsearch", 8: "tables merge barrier", 11: "tables 2 rank",
                 12: "tables 3 merge", 13: "tables 4 leaves", 14: "tables 5 codes", 15: "tables 6 header"},
     "entropy": {0: "emit tables+sort", 4: "emit block load+zigzag", 5: "emit walk", 1: "emit scan",
-                2: "emit windows+store", 3: "emit ff/edges"},
+                2: "emit windows+store", 3: "emit ff/edges", 6: "emit summary+arrival",
+                7: "emit tail bits/edges+scan", 8: "emit tail ff loads+bytes", 9: "emit tail byte scan",
+                10: "emit tail stores"},
 }
 
 
