@@ -60,6 +60,9 @@ constexpr int kStuffPass = 4096;
 #ifndef DMMT_TAIL_DMA
 #define DMMT_TAIL_DMA 1  // fused offsets: the packed 0xFF counts land in LDS with the first loads (0: study builds)
 #endif
+#ifndef DMMT_TAIL_NSEG1
+#define DMMT_TAIL_NSEG1 1  // fused offsets: no chunk_span division per chunk without restart intervals (0: study builds)
+#endif
 #ifndef DMMT_EMIT_PRIO
 #define DMMT_EMIT_PRIO 1  // k_emit's wave priorities by walk length (0: off, study builds)
 #endif
@@ -719,14 +722,19 @@ __device__ __forceinline__ void fused_offsets(const uint32_t* __restrict__ cbits
         const uint32_t nlast = ld_agent(cbits + cl), elast = ld_agent(cedge + cl);
         uint32_t firstm = 0, seglm = 0;  // per chunk i: bit i
 #pragma unroll
-        for (int i = 0; i < KP; ++i) {
-            const int c = c0 + i;
-            if (c < c1) {
-                const ChunkSpan sp = chunk_span(g, c);
-                firstm |= (uint32_t)sp.seg_first << i;
-                seglm |= (uint32_t)sp.seg_last << i;
-            } else {
-                nbits[i] = 0u;
+        for (int i = 0; i < KP; ++i) nbits[i] = c0 + i < c1 ? nbits[i] : 0u;
+        if (DMMT_TAIL_NSEG1 && g.nseg == 1) {  // (uniform) one segment: only chunk 0 starts it, only the frame's last ends it
+            firstm = c0 == 0 && c0 < c1 ? 1u : 0u;
+            seglm = c1 == nch && c0 < c1 ? 1u << (c1 - 1 - c0) : 0u;
+        } else {
+#pragma unroll
+            for (int i = 0; i < KP; ++i) {
+                const int c = c0 + i;
+                if (c < c1) {
+                    const ChunkSpan sp = chunk_span(g, c);
+                    firstm |= (uint32_t)sp.seg_first << i;
+                    seglm |= (uint32_t)sp.seg_last << i;
+                }
             }
         }
         bool f = false;

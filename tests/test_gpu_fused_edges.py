@@ -146,3 +146,28 @@ def test_fused_tables_u64_keys(encoder):
     opts = _opts(sub, 90)
     ref = oracle.encode_coefficients(coef, w, h, sub, luma, chroma)
     assert encoder.encode_coefficients(coef, w, h, opts) == ref
+
+
+@pytest.mark.parametrize("sub,w,h", [(0, 264, 256), (2, 528, 512)])
+def test_fused_offsets_ff_counts_past_a_byte(encoder, sub, w, h):
+    """k_emit's fused offsets read each chunk's 0xFF counts packed one byte each
+    (global_load_lds into LDS with the first loads) and take the full count from
+    chunk_ff where the byte holds 255.  Crafted blocks: every AC coefficient of the
+    first blocks 32767 (category 15, fifteen 1-bits of extra bits after a one-bit
+    code: about one 0xFF byte per coefficient at every alignment, thousands per
+    chunk), the rest sparse noise (counts below 255), an odd number of chunks (the
+    last 16-byte piece reads the padding).  [binary_stream.rs:38-96,
+    segment_marker_injector.rs:13-30]"""
+    nl = 1 if sub == 0 else 4
+    mcus = (w // (8 * (1 if sub == 0 else 2))) * (h // (8 * (1 if sub == 0 else 2)))
+    nb = mcus * (nl + 2)
+    assert _chunks(w, h, sub) % 2 == 1
+    rng = np.random.default_rng(255)
+    coef = np.where(rng.random((nb, 64)) < 0.05, rng.integers(-20, 21, (nb, 64)), 0).astype(np.int16)
+    heavy = nb // 2
+    coef[:heavy, 1:] = 32767
+    coef[:heavy, 0] = 0
+    luma, chroma = dmmt_jpeg.quality_tables(75)
+    ref = oracle.encode_coefficients(coef, w, h, sub, luma, chroma)
+    assert ref.count(b"\xff\x00") > 4 * 255 * _chunks(w, h, sub) // 2
+    assert encoder.encode_coefficients(coef, w, h, _opts(sub, 75)) == ref
