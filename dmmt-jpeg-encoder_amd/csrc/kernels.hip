@@ -1075,6 +1075,9 @@ __global__ __launch_bounds__(512) void k_tables(const uint32_t* __restrict__ ac_
 //  6 the DHT segment, and for table 0 the rest of the header (write_table_header)
 // One barrier: before 6 (every table's symbol count).  LDS per table (bytes):
 // F u32[cap] | the keys u64[cap] | Sym u8[cap]; cap = 256 for the AC tables, 16 DC.
+#ifndef DMMT_TAIL_SORT2
+#define DMMT_TAIL_SORT2 1  // an AC table of at most 128 symbols sorted in two register slots (0: study builds)
+#endif
 constexpr int kTailLevels = 15;
 constexpr int kTailBase[4] = {0, 208, 3536, 3744};
 static_assert(kTailBase[3] + 3328 == kTailLdsBytes, "tables_tail's LDS regions");
@@ -1291,13 +1294,30 @@ __device__ __forceinline__ void tables_tail(uint8_t* lds, const uint32_t* ac_his
     // ---- 2: the present keys in ascending order (absent symbols: kMergeInf, last)
     // -> F (frequency), Sym by leaf rank
     if (k32) {
-        if (ac) {
+        if (ac && (!DMMT_TAIL_SORT2 || n > 128)) {
             uint32_t x[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) x[q] = f[q] ? (f[q] << 8) | (uint32_t)(lane + 64 * q) : kMergeInf;
             sort_bitonic<4>(x);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
+                if (lane + 64 * q < n) {
+                    F[lane + 64 * q] = x[q] >> 8;
+                    Sym[lane + 64 * q] = (uint8_t)x[q];
+                }
+        } else if (ac) {  // (uniform) at most 128 present symbols: compacted into two slots, half the network
+            uint32_t* const K32 = reinterpret_cast<uint32_t*>(Key);
+            int at = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (f[q]) K32[at + __popcll(pres[q] & ((1ull << lane) - 1ull))] = (f[q] << 8) | (uint32_t)(lane + 64 * q);
+                at += __popcll(pres[q]);
+            }
+            wave_lds_sync();
+            uint32_t x[2] = {lane < n ? K32[lane] : kMergeInf, lane + 64 < n ? K32[lane + 64] : kMergeInf};
+            sort_bitonic<2>(x);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
                 if (lane + 64 * q < n) {
                     F[lane + 64 * q] = x[q] >> 8;
                     Sym[lane + 64 * q] = (uint8_t)x[q];
