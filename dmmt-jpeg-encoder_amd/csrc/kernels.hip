@@ -1538,6 +1538,9 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 // the 15 levels a package can sum over stay below 2^30 (a key weight << 1 | tag
 // stays below its merge's padding); stripes keep k_tables
 // (their histograms are summed on the host first)
+#ifndef DMMT_HIST_WG_CAP
+#define DMMT_HIST_WG_CAP 1024  // k_hist workgroups per launch (study builds: other caps)
+#endif
 bool tables_fusable(const Geom& g) { return g.stripe_first && !g.more_after && g.bpf * 64 * 16 < (1ll << 30); }
 
 hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st, bool fuse_tables,
@@ -1545,7 +1548,7 @@ hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat
     // at most 1024 workgroups (4K: 1.5 blocks per thread): fewer histogram
     // flushes; 4K q90 bench 157.5 -> 159.6 Gpx/s, 8K 4:2:0 296.6 -> 299.0 against
     // one block per thread (512: faster pipelined still, but k_hist alone +4 us)
-    const int per_frame = 1024 / n_frames > 0 ? 1024 / n_frames : 1;
+    const int per_frame = DMMT_HIST_WG_CAP / n_frames > 0 ? DMMT_HIST_WG_CAP / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
     const bool fuse = fuse_tables && tables_fusable(g);
     auto go = [&](auto kern) {
