@@ -2,7 +2,9 @@
 // stuffing.  [encoder.rs:264-404 write_image_data / write_{dc,ac}_from_block,
 // binary_stream.rs:38-96 BitWriter, segment_marker_injector.rs:13-30]
 //
-// Three launches, no inter-workgroup waiting anywhere:
+// Three kernels, no inter-workgroup waiting anywhere (two launches for frames of
+// at most kFusedOffsetsMaxChunks chunks, whose k_offsets work runs in k_emit's
+// last workgroup: fused_offsets):
 //  k_emit        one workgroup per chunk of kChunkBlocks blocks, one thread per
 //                block: the bits of every block (a register walk), a workgroup
 //                scan for the block offsets inside the chunk, every code placed
@@ -10,8 +12,8 @@
 //                which goes to the chunk's staging slot.  Per chunk it also
 //                records its bit count, its first and last 16 bits and, for each
 //                of the 8 residues the chunk's start can have modulo 8, the 0xFF
-//                bytes lying wholly inside it -- so no later pass re-reads the
-//                stream to count them.
+//                bytes lying wholly inside it (also packed one byte each for the
+//                fused offsets) -- so no later pass re-reads the stream to count them.
 //  k_offsets     one workgroup per frame: segmented scan of the chunk bit counts
 //                (every chunk's bit offset in its restart segment); each chunk's
 //                output bytes -- its bytes, a 0x00 per 0xFF (k_emit's count at its
