@@ -43,6 +43,10 @@ constexpr int kPpmThreads = 256;
 constexpr int kPpmChunk = kPpmWin * kPpmThreads;  // bytes per workgroup
 constexpr int kPpmTail = 256;                  // bytes staged past the chunk for tokens running on
 constexpr int kPpmCarryThreads = 1024;
+#ifndef DMMT_PPM_U8_SHORT
+#define DMMT_PPM_U8_SHORT 1  // 8-bit bodies: tokens of four or more bytes go to the general path (0: study builds)
+#endif
+
 // comment-free path: a chunk is kFastPieces 16-byte pieces per thread (8 KB: the
 // parse kernel's LDS of 16.5 KB keeps 8 workgroups per CU); the count kernel
 // takes kCountChunks chunks per workgroup (4 pieces per thread)
@@ -533,6 +537,11 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
         uint32_t st[P][4], sg[P][4], wnext[P];
         uint32_t n01 = 0;  // starts per piece, two 16-bit fields
         uint32_t lm = 0;   // token starts followed by three more token bytes (tokens of 4+ bytes)
+        // 8-bit samples: a valid token has 1-3 digits unless it carries leading zeros,
+        // which no P3 writer emits, so the run-of-four test is left out and a token of
+        // four or more bytes is caught in the token loop instead (the body then goes
+        // down the general path, as a comment's would)
+        constexpr bool kShortOnly = sizeof(Out) == 1 && DMMT_PPM_U8_SHORT;
 #pragma unroll
         for (int q = 0; q < P; ++q) {
 #pragma unroll
@@ -552,17 +561,19 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                 }
             }
             uint32_t nq = 0;
-            const uint32_t sgn = sig_bytes(wnext[q]);
+            const uint32_t sgn = kShortOnly ? 0u : sig_bytes(wnext[q]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 st[q][k] = starts_of(sg[q][k], prev);
                 prev = sg[q][k];
                 nq += (uint32_t)__popc(st[q][k]);
-                // byte j of run4: bytes j .. j + 3 are all token bytes
-                const uint32_t nb = k < 3 ? sg[q][k + 1] : sgn, g = sg[q][k];
-                const uint32_t run4 = g & __builtin_amdgcn_alignbyte(nb, g, 1u) & __builtin_amdgcn_alignbyte(nb, g, 2u) &
-                                      __builtin_amdgcn_alignbyte(nb, g, 3u);
-                lm |= st[q][k] & run4;
+                if constexpr (!kShortOnly) {
+                    // byte j of run4: bytes j .. j + 3 are all token bytes
+                    const uint32_t nb = k < 3 ? sg[q][k + 1] : sgn, g = sg[q][k];
+                    const uint32_t run4 = g & __builtin_amdgcn_alignbyte(nb, g, 1u) &
+                                          __builtin_amdgcn_alignbyte(nb, g, 2u) & __builtin_amdgcn_alignbyte(nb, g, 3u);
+                    lm |= st[q][k] & run4;
+                }
             }
             n01 |= nq << (16 * q);
         }
@@ -625,7 +636,7 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
                 }
             }
         };
-        if (__ballot(lm != 0u))  // (uniform)
+        if (!kShortOnly && __ballot(lm != 0u))  // (uniform)
             compact(std::true_type{});
         else
             compact(std::false_type{});
@@ -641,7 +652,10 @@ __global__ __launch_bounds__(kPpmThreads) void k_ppm_fast(PpmText t, PpmReport* 
             uint32_t v[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = short_token(e[j]);
-            if ((e[0] | e[1] | e[2] | e[3]) & 0x80000000u) {  // four or more bytes (u16 samples, leading zeros)
+            if constexpr (kShortOnly) {  // no byte below '0' among an entry's four: four or more bytes
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bad |= (((e[j] | 0x80808080u) - 0x30303030u) & 0x80808080u) == 0x80808080u;
+            } else if ((e[0] | e[1] | e[2] | e[3]) & 0x80000000u) {  // four or more bytes (u16 samples, leading zeros)
 #pragma unroll 1
                 for (int j = 0; j < 4; ++j) {
                     const uint32_t ej = j == 0 ? e[0] : j == 1 ? e[1] : j == 2 ? e[2] : e[3];
