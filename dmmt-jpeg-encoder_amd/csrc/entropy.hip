@@ -62,9 +62,6 @@ constexpr int kStuffPass = 4096;
 #ifndef DMMT_TAIL_DMA
 #define DMMT_TAIL_DMA 1  // fused offsets: the packed 0xFF counts land in LDS with the first loads (0: study builds)
 #endif
-#ifndef DMMT_STUFF_BRANCHFREE
-#define DMMT_STUFF_BRANCHFREE 1  // k_stuffwrite stages whole lanes without a branch per byte (0: study builds)
-#endif
 #ifndef DMMT_TAIL_NSEG1
 #define DMMT_TAIL_NSEG1 1  // fused offsets: no chunk_span division per chunk without restart intervals (0: study builds)
 #endif
@@ -950,8 +947,7 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
                                                     uint8_t* __restrict__ out, size_t out_stride,
                                                     uint32_t* __restrict__ out_len, int* __restrict__ status) {
     __shared__ uint32_t sWave[4];
-    // the staged pass, then one dummy word per lane (stuffing bytes that are not there)
-    __shared__ __attribute__((aligned(16))) uint8_t sOut[2 * kStuffPass + 16 + 4 * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t sOut[2 * kStuffPass + 16];
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const int frame = blockIdx.y;
     const int c = blockIdx.x;
@@ -1078,21 +1074,7 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
         const uint32_t ffs = sWave[0] + sWave[1] + sWave[2] + sWave[3];
         // stage the stuffed pass in LDS, then store it with consecutive lanes on
         // consecutive bytes (coalesced)
-        if (nvalid == 16 && DMMT_STUFF_BRANCHFREE) {
-            // every lane but the chunk's last: no branch per byte -- the 0x00 after a
-            // byte goes to the next place when the byte is 0xFF, else to this lane's
-            // dummy word past the staged pass
-            uint32_t dst = delta + (uint32_t)tid * 16u + pre;
-            const uint32_t dummy = 2u * kStuffPass + 16u + 4u * (uint32_t)lane;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t b = (x[j >> 2] >> (24 - 8 * (j & 3))) & 0xFFu;
-                const bool ff = b == 0xFFu;
-                sOut[dst] = (uint8_t)b;
-                sOut[ff ? dst + 1u : dummy] = 0x00;
-                dst += ff ? 2u : 1u;
-            }
-        } else if (nvalid) {
+        if (nvalid) {
             uint32_t dst = delta + (uint32_t)tid * 16u + pre;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
