@@ -5,6 +5,7 @@ dmmt_parse_ppm) and the same error variant, whatever the whitespace, comments
 (a '#' comment runs to its '\\n' and does not end a token), '+' signs, leading
 zeros, chunk boundaries (4096-byte chunks) and buffer alignment."""
 import os
+import re
 
 import numpy as np
 import pytest
@@ -353,6 +354,34 @@ def test_convert_device_batch_redoes_only_the_failing_file(encoder, spec_tables)
                 assert encoder.d2h(d_out, size) == oracle.encode(rgb, 255, 2, *spec_tables)
     finally:
         encoder.set_lanes(1)
+        for p in allocs:
+            encoder.free(p)
+
+
+def test_convert_device_batch_leading_zeros_8bit(encoder, spec_tables):
+    """An 8-bit body with leading zeros ("007", tokens of four or more bytes): the
+    comment-free pass for 8-bit samples does not parse such tokens, flags them and the
+    file is redone on its own on the general path -- its samples and JPEG exactly the
+    oracle's; the clean files of the batch are not redone [ppm.rs:41-77, 247-251:
+    str::parse::<u16> accepts leading zeros]"""
+    rng = np.random.default_rng(77)
+    cases = []
+    for k in range(6):
+        rgb = rng.integers(0, 256, (20 + k, 36, 3), dtype=np.uint8)
+        cases.append((p3_text(rgb, 255, rng, zeros=0.05 if k == 2 else 0.0), rgb))
+    assert re.search(rb"\s0[0-9]", cases[2][0])  # (a token with a leading zero)
+    allocs = []
+    try:
+        files = _device_files(encoder, [d for d, _ in cases], allocs)
+        codes = encoder.convert_ppm_device_batch(files, dmmt_jpeg.JpegTransformationOptions())
+        assert codes == [0] * len(cases)
+        assert encoder.batch_redone() == 1
+        for (d_text, n, hdr, d_out, cap, d_len), (data, rgb) in zip(files, cases):
+            size = int(np.frombuffer(encoder.d2h(d_len, 4), np.uint32)[0])
+            assert encoder.d2h(d_out, size) == oracle.encode(rgb, 255, 2, *spec_tables)
+        got, mx = decode_gpu(encoder, cases[2][0])
+        assert mx == 255 and np.array_equal(got, cases[2][1])
+    finally:
         for p in allocs:
             encoder.free(p)
 
