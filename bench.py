@@ -829,6 +829,10 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
         ppm_jpeg = ppm_to_jpeg(enc, w, h, opts, opt_c, args.ppm_steps) if args.ppm_steps > 0 and fps == 1 else None
         ppm_stream = (ppm_to_jpeg_stream(enc, w, h, opt_c, max(2, args.ppm_steps // 4), lanes)
                       if args.ppm_steps > 0 and fps == 1 else None)
+        # one file per call through the same API: decode and encode back to back,
+        # one synchronisation (the report checked after it), one lane
+        ppm_one = (ppm_to_jpeg_stream(enc, w, h, opt_c, args.ppm_steps, 1, distinct=1, per_call=1)
+                   if args.ppm_steps > 0 and fps == 1 else None)
         cpu = None
         if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
             from oracle.synth import synthetic  # numpy twin of the device generator
@@ -886,6 +890,7 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
             "cpu_baseline": cpu,
             "ppm_ingest": ingest,
             "ppm_to_jpeg": ppm_jpeg,
+            "ppm_to_jpeg_one_call": ppm_one,
             "ppm_to_jpeg_stream": ppm_stream,
         }
     for p in d_in + d_out + d_len:
