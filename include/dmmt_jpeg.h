@@ -294,7 +294,8 @@ int dmmt_convert_ppm_to_jpeg(dmmt_ctx* ctx, const char* input_path, const char* 
  * decoded and encoded back to back over the context's lanes (dmmt_ctx_set_lanes), with no
  * synchronisation between files: a P3 body is decoded on the comment-free path on the
  * assumption that it has no '#' and no error, and encoded at once; its report is checked
- * after the batch, and a file whose body needs the general path (a comment, a '+' sign),
+ * after the batch, and a file whose body needs the general path (a comment, a '+' sign,
+ * an 8-bit sample written with leading zeros),
  * or that fails (its own decode report or its own encode's error words), is redone on its
  * own.  codes[i] receives file i's result: the code dmmt_decode_ppm_device and then the
  * encode would return for it (a failed file's size is 0).  Returns the first non-zero code,
