@@ -47,7 +47,10 @@ static __device__ unsigned long long g_trace[64];
 static_assert(kChunkBlocks == 256 || kChunkBlocks == 512, "one thread per block, one workgroup per chunk");
 constexpr int kEmitThreads = kChunkBlocks;
 constexpr int kEmitWaves = kEmitThreads / 64;
-constexpr int kEmitOcc = kChunkBlocks == 256 ? 7 : 3;  // workgroups per CU
+#ifndef DMMT_EMIT_OCC
+#define DMMT_EMIT_OCC 7  // k_emit workgroups per CU the launch bounds target (256-block chunks; study builds: others)
+#endif
+constexpr int kEmitOcc = kChunkBlocks == 256 ? DMMT_EMIT_OCC : 3;  // workgroups per CU
 
 // LDS word window of k_emit: 32 Ki bits = 128 bits per block on average (the 4K
 // q90 workload averages ~110).  A chunk with more is assembled in several
