@@ -386,7 +386,7 @@ int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bit
     }
     {
         StageTimer t(c, ST_EMIT, st);
-        HIP_TRY(launch_emit(nf, g, w, true, st));
+        HIP_TRY(launch_emit(nf, g, w, true, st, c->nlanes <= 1));
     }
     if (!offsets_fusable(g)) {  // (else k_emit's last workgroup computed them)
         StageTimer t(c, ST_OFFSETS, st);
@@ -1579,7 +1579,7 @@ extern "C" int dmmt_stripe_measure(dmmt_ctx* c, const uint64_t hist_sum[DMMT_STR
     }
     {
         StageTimer t(c, ST_EMIT, s);
-        HIP_TRY(launch_emit(1, g, w, false, s));  // (the joined stripe's offsets wait for its seam: dmmt_stripe_write)
+        HIP_TRY(launch_emit(1, g, w, false, s, c->nlanes <= 1));  // (the joined stripe's offsets wait for its seam: dmmt_stripe_write)
     }
     std::vector<uint32_t> nb((size_t)g.nch), edge((size_t)g.nch);
     HIP_TRY(hipMemcpyAsync(nb.data(), w.chunk_bits, nb.size() * 4, hipMemcpyDeviceToHost, s));

@@ -68,6 +68,9 @@ constexpr int kStuffPass = 4096;
 #ifndef DMMT_TAIL_NSEG1
 #define DMMT_TAIL_NSEG1 1  // fused offsets: no chunk_span division per chunk without restart intervals (0: study builds)
 #endif
+#ifndef DMMT_EMIT_PRIO_ALWAYS
+#define DMMT_EMIT_PRIO_ALWAYS 0  // study builds: the priorities with several lanes too (the round-5 behaviour)
+#endif
 #ifndef DMMT_EMIT_PRIO
 #define DMMT_EMIT_PRIO 1  // k_emit's wave priorities by walk length (0: off, study builds)
 #endif
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
                                               unsigned long long* __restrict__ chunk_bit0,
                                               unsigned long long* __restrict__ chunk_out,
                                               unsigned long long* __restrict__ total_out,
-                                              unsigned long long* __restrict__ chunk_ff8) {
+                                              unsigned long long* __restrict__ chunk_ff8, int prio) {
     // code tables: [luma AC 256][chroma AC 256][luma DC 16][chroma DC 16]
     __shared__ uint2 sTab[2 * 256 + 2 * 16];
     // the window image; during the sort and the walk its first words hold the
@@ -401,10 +404,14 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         // The waves walk sorted blocks, the heaviest last, and every wave of the
         // workgroup waits for the slowest at the barrier after the walk: the longer a
         // wave's walk, the higher its issue priority on its SIMD (4K q90, one lane:
-        // k_emit 27.0 -> 23.1 us; pipelined throughput unchanged)
-        if (wave == 3) __builtin_amdgcn_s_setprio(3);
-        else if (wave == 2) __builtin_amdgcn_s_setprio(2);
-        else if (wave == 1) __builtin_amdgcn_s_setprio(1);
+        // k_emit 27.0 -> 23.1 us).  Only when the context runs one lane (prio): with
+        // several, the raised waves take issue slots from the other lanes' kernels,
+        // -1.5 % on the settled 4-lane bench (profiles/r06_emit_prio_ab.txt)
+        if (prio) {  // (uniform)
+            if (wave == 3) __builtin_amdgcn_s_setprio(3);
+            else if (wave == 2) __builtin_amdgcn_s_setprio(2);
+            else if (wave == 1) __builtin_amdgcn_s_setprio(1);
+        }
 #endif
         // one walk: the block's bits into this thread's private slot, and its bit count
         if (valid) {
@@ -428,7 +435,7 @@ __global__ __launch_bounds__(kEmitThreads, kEmitOcc) void k_emit(const int16_t* 
         }
     }
 #if DMMT_EMIT_PRIO
-    __builtin_amdgcn_s_setprio(0);
+    if (prio) __builtin_amdgcn_s_setprio(0);
 #endif
     // a block too long for its slot sends the whole chunk down the re-walk path
     const bool over = __syncthreads_or(slot_over) != 0;
@@ -1108,12 +1115,12 @@ __global__ __launch_bounds__(256, 8) void k_stuffwrite(const uint32_t* __restric
 // --------------------------------------------------------------------- launchers
 bool offsets_fusable(const Geom& g) { return g.nch <= kFusedOffsetsMaxChunks; }
 
-hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_offsets, hipStream_t st) {
+hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_offsets, hipStream_t st, bool prio) {
     const int fuse = fuse_offsets && offsets_fusable(g) ? 1 : 0;
     hipLaunchKernelGGL(k_emit, dim3(g.nch, n_frames), dim3(kEmitThreads), 0, st, (const int16_t*)w.coef,
                        (const int16_t*)w.dcdiff, (const uint8_t*)w.lastnz, (const uint32_t*)w.code_tab, g, w.stage, w.chunk_bits, w.chunk_ff,
                        w.chunk_edge, w.ac_hist, w.dc_hist, fuse, w.arrive, w.chunk_bit0, w.chunk_out, w.total_out,
-                       w.chunk_ff8);
+                       w.chunk_ff8, prio || DMMT_EMIT_PRIO_ALWAYS ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -52,7 +52,9 @@ constexpr int kFusedRoundChunks = 1536;       // per round of the fused scan (4K
 constexpr int kFusedOffsetsMaxChunks = 4 * kFusedRoundChunks;  // (8K 4:2:0: 3038 chunks, two rounds)
 constexpr int kArriveFrameWords = 65 * 32;  // k_emit's arrival counters per frame (Work::arrive)
 bool offsets_fusable(const Geom& g);
-hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_offsets, hipStream_t st);
+// prio: k_emit's heavier waves raise their issue priority (a context of one lane:
+// shorter frames; with several lanes it costs the others' kernels issue slots)
+hipError_t launch_emit(int n_frames, const Geom& g, const Work& w, bool fuse_offsets, hipStream_t st, bool prio);
 hipError_t launch_offsets(int n_frames, const Geom& g, const Work& w, hipStream_t st);
 hipError_t launch_stuffwrite(int n_frames, const Geom& g, const Work& w, uint8_t* out, size_t out_stride,
                              uint32_t* out_len, hipStream_t st);
