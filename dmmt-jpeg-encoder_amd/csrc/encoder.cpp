@@ -378,7 +378,8 @@ int enqueue_back_half(dmmt_ctx* c, const Geom& g, int nf, const Work& w, int bit
     const bool fused_tables = !hist_done && c->fuse_tables && tables_fusable(g);
     if (!hist_done) {
         StageTimer t(c, ST_HIST, st);
-        HIP_TRY(launch_hist(nf, g, w, check_cat, st, fused_tables, bits, out, out_stride));
+        HIP_TRY(launch_hist(nf, g, w, check_cat, st, fused_tables, bits, out, out_stride,
+                            c->nlanes > 1 ? DMMT_HIST_WG_CAP_LANES : 0));
     }
     if (!fused_tables) {
         StageTimer t(c, ST_TABLES, st);

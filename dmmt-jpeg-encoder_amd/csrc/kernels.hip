@@ -1544,11 +1544,12 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 bool tables_fusable(const Geom& g) { return g.stripe_first && !g.more_after && g.bpf * 64 * 16 < (1ll << 30); }
 
 hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st, bool fuse_tables,
-                       int bits_per_channel, uint8_t* out, size_t out_stride) {
+                       int bits_per_channel, uint8_t* out, size_t out_stride, int wg_cap) {
     // at most 1024 workgroups (4K: 1.5 blocks per thread): fewer histogram
     // flushes; 4K q90 bench 157.5 -> 159.6 Gpx/s, 8K 4:2:0 296.6 -> 299.0 against
     // one block per thread (512: faster pipelined still, but k_hist alone +4 us)
-    const int per_frame = DMMT_HIST_WG_CAP / n_frames > 0 ? DMMT_HIST_WG_CAP / n_frames : 1;
+    const int cap = wg_cap > 0 ? wg_cap : DMMT_HIST_WG_CAP;
+    const int per_frame = cap / n_frames > 0 ? cap / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);
     const bool fuse = fuse_tables && tables_fusable(g);
     auto go = [&](auto kern) {

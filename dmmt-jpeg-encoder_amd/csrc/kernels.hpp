@@ -40,9 +40,13 @@ hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_b
 // fuse_tables: when tables_fusable(g), the frame's last k_hist workgroup also does
 // launch_tables' work (code tables, header into out), and no launch_tables follows
 bool tables_fusable(const Geom& g);
+// wg_cap: at most this many workgroups per launch (0: the default, DMMT_HIST_WG_CAP)
 hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat, hipStream_t st,
                        bool fuse_tables = false, int bits_per_channel = 8, uint8_t* out = nullptr,
-                       size_t out_stride = 0);
+                       size_t out_stride = 0, int wg_cap = 0);
+#ifndef DMMT_HIST_WG_CAP_LANES
+#define DMMT_HIST_WG_CAP_LANES 0  // k_hist's cap when the context runs several lanes (0: the default; study builds)
+#endif
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st);
 // fuse_offsets: when offsets_fusable(g), k_emit's last workgroup per frame also
