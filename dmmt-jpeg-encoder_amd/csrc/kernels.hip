@@ -1547,7 +1547,10 @@ hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat
                        int bits_per_channel, uint8_t* out, size_t out_stride, int wg_cap) {
     // at most 1024 workgroups (4K: 1.5 blocks per thread): fewer histogram
     // flushes; 4K q90 bench 157.5 -> 159.6 Gpx/s, 8K 4:2:0 296.6 -> 299.0 against
-    // one block per thread (512: faster pipelined still, but k_hist alone +4 us)
+    // one block per thread.  512 is faster pipelined still but k_hist alone +4 us,
+    // so a context of several lanes passes wg_cap = DMMT_HIST_WG_CAP_LANES (512:
+    // settled 4-lane bench +2.4 %, profiles/r06_hist_cap_lanes_ab.txt) and one lane
+    // keeps the default
     const int cap = wg_cap > 0 ? wg_cap : DMMT_HIST_WG_CAP;
     const int per_frame = cap / n_frames > 0 ? cap / n_frames : 1;
     dim3 grid(clampi((g.bpf + 255) / 256, 1, per_frame), n_frames);

@@ -45,7 +45,7 @@ hipError_t launch_hist(int n_frames, const Geom& g, const Work& w, int check_cat
                        bool fuse_tables = false, int bits_per_channel = 8, uint8_t* out = nullptr,
                        size_t out_stride = 0, int wg_cap = 0);
 #ifndef DMMT_HIST_WG_CAP_LANES
-#define DMMT_HIST_WG_CAP_LANES 0  // k_hist's cap when the context runs several lanes (0: the default; study builds)
+#define DMMT_HIST_WG_CAP_LANES 512  // k_hist's cap when the context runs several lanes (profiles/r06_hist_cap_lanes_ab.txt)
 #endif
 hipError_t launch_tables(int n_frames, const Geom& g, const Work& w, int bits_per_channel, uint8_t* out,
                          size_t out_stride, hipStream_t st);
