@@ -404,7 +404,7 @@ int enqueue_direct(dmmt_ctx* c, const void* d_rgb, size_t frame_stride, int sb, 
                    const Work& w, int bits, uint8_t* out, size_t out_stride, uint32_t* out_len, hipStream_t st) {
     {
         StageTimer t(c, ST_FRONT, st);
-        HIP_TRY(launch_front(d_rgb, frame_stride, sb, nf, g, w, st));
+        HIP_TRY(launch_front(d_rgb, frame_stride, sb, nf, g, w, st, c->nlanes > 1 ? DMMT_FRONT_PER_CU_LANES : 0));
     }
     return enqueue_back_half(c, g, nf, w, bits, out, out_stride, out_len, st, sb == 4);
 }

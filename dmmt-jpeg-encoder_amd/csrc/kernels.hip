@@ -1485,11 +1485,12 @@ constexpr int front_wpe() {
 
 template <int HR, int VR, typename S>
 static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const Geom& g, const Work& w,
-                       hipStream_t st) {
+                       hipStream_t st, int per_cu_cap) {
     constexpr int TM = 32 / HR;
     const long long ntiles = (long long)((g.mcux + TM - 1) / TM) * g.mcuy;
     // one workgroup per resident slot: each loops over tiles, prefetching the next
-    static int resident = 0;
+    static int resident = 0, n_cus = 0;
+    static bool per_cu_env = false;
     if (!resident) {
         int per_cu = 0, dev = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_front<HR, VR, S, front_wpe<HR, VR, S>()>, 256, 0) != hipSuccess ||
@@ -1498,38 +1499,44 @@ static void front_impl(const void* rgb, size_t stride_elems, int n_frames, const
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
             cus = 256;
-        if (const char* e = getenv("DMMT_FRONT_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;  // tuning knob
+        if (const char* e = getenv("DMMT_FRONT_PER_CU")) {  // tuning knob (both lane modes)
+            per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+            per_cu_env = true;
+        }
         resident = per_cu * cus;
+        n_cus = cus;
     }
-    dim3 grid(clampi(ntiles, 1, resident / n_frames > 0 ? resident / n_frames : 1), n_frames);
+    // per_cu_cap: fewer resident workgroups per CU (a context of several lanes)
+    const int res = per_cu_cap > 0 && !per_cu_env ? std::min(resident, per_cu_cap * n_cus) : resident;
+    dim3 grid(clampi(ntiles, 1, res / n_frames > 0 ? res / n_frames : 1), n_frames);
     hipLaunchKernelGGL((k_front<HR, VR, S, front_wpe<HR, VR, S>()>), grid, dim3(256), 0, st, (const S*)rgb, stride_elems, g, w.norm_lut,
                        w.qtab, w.coef, w.status);
 }
 
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
-                        const Work& w, hipStream_t st) {
+                        const Work& w, hipStream_t st, int per_cu_cap) {
     const size_t se = frame_stride_bytes / (size_t)sample_bytes;
     if (sample_bytes == 4) {
         if (g.hr == 1)
-            front_impl<1, 1, float>(rgb, se, n_frames, g, w, st);
+            front_impl<1, 1, float>(rgb, se, n_frames, g, w, st, per_cu_cap);
         else if (g.vr == 1)
-            front_impl<2, 1, float>(rgb, se, n_frames, g, w, st);
+            front_impl<2, 1, float>(rgb, se, n_frames, g, w, st, per_cu_cap);
         else
-            front_impl<2, 2, float>(rgb, se, n_frames, g, w, st);
+            front_impl<2, 2, float>(rgb, se, n_frames, g, w, st, per_cu_cap);
     } else if (sample_bytes == 1) {
         if (g.hr == 1)
-            front_impl<1, 1, uint8_t>(rgb, se, n_frames, g, w, st);
+            front_impl<1, 1, uint8_t>(rgb, se, n_frames, g, w, st, per_cu_cap);
         else if (g.vr == 1)
-            front_impl<2, 1, uint8_t>(rgb, se, n_frames, g, w, st);
+            front_impl<2, 1, uint8_t>(rgb, se, n_frames, g, w, st, per_cu_cap);
         else
-            front_impl<2, 2, uint8_t>(rgb, se, n_frames, g, w, st);
+            front_impl<2, 2, uint8_t>(rgb, se, n_frames, g, w, st, per_cu_cap);
     } else {
         if (g.hr == 1)
-            front_impl<1, 1, uint16_t>(rgb, se, n_frames, g, w, st);
+            front_impl<1, 1, uint16_t>(rgb, se, n_frames, g, w, st, per_cu_cap);
         else if (g.vr == 1)
-            front_impl<2, 1, uint16_t>(rgb, se, n_frames, g, w, st);
+            front_impl<2, 1, uint16_t>(rgb, se, n_frames, g, w, st, per_cu_cap);
         else
-            front_impl<2, 2, uint16_t>(rgb, se, n_frames, g, w, st);
+            front_impl<2, 2, uint16_t>(rgb, se, n_frames, g, w, st, per_cu_cap);
     }
     return hipGetLastError();
 }

@@ -33,8 +33,13 @@ struct Work {
 
 enum Stage { ST_FRONT = 0, ST_HIST, ST_TABLES, ST_EMIT, ST_OFFSETS, ST_STUFFWRITE, ST_COUNT };
 
+// per_cu_cap: at most this many resident k_front workgroups per CU (0: as many as
+// fit, 4); a context of several lanes passes DMMT_FRONT_PER_CU_LANES
 hipError_t launch_front(const void* rgb, size_t frame_stride_bytes, int sample_bytes, int n_frames, const Geom& g,
-                        const Work& w, hipStream_t st);
+                        const Work& w, hipStream_t st, int per_cu_cap = 0);
+#ifndef DMMT_FRONT_PER_CU_LANES
+#define DMMT_FRONT_PER_CU_LANES 2  // k_front workgroups per CU with several lanes (profiles/r06_front_per_cu_lanes_ab.txt)
+#endif
 // DC differences, AC and DC histograms, last non-zero positions of the blocks in
 // w.coef (check_cat: an AC -32768, which has no category, can occur)
 // fuse_tables: when tables_fusable(g), the frame's last k_hist workgroup also does
