@@ -797,6 +797,9 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
     elapsed = timed(lanes)
     if args.roofline_order == "last":
         single, prof = roofline_pass()
+    # the same one-lane steps without the event records: a frame's latency on the
+    # production path (the roofline pass's 8 event records per frame stretch it)
+    single_plain = timed(1)
     extra = {}
     if args.mall_compare:  # inputs resident in the Infinity Cache: 4 slots
         extra["mall_resident_4_slots"] = timed(lanes, min(4, nslots))
@@ -854,6 +857,7 @@ def main(argv=None, make_encoder=None, emit=None, make_group=None):
         # the roofline pass's wall time: one frame at a time, events on (the latency of
         # a frame plus the event records)
         cfg["single_lane_ms_per_step"] = round(single / args.steps * 1e3, 4)
+        cfg["single_lane_plain_ms_per_step"] = round(single_plain / args.steps * 1e3, 4)
         line = {
             "metric": "Mpixel/s encoded (4K PPM, q=90)" if args.config == "4k444q90" else f"Mpixel/s encoded ({args.config})",
             "value": round(value, 2),

@@ -144,8 +144,8 @@ def test_bench_two_ranks_gloo(tmp_path):
     f0 = {tuple(x[2:]) for x in r0["log"] if x[0] == "frames"}
     f1 = {tuple(x[2:]) for x in r1["log"] if x[0] == "frames"}
     # untimed settle steps, then the timed steps, pipelined over the default lanes, then one at a
-    # time with events (roofline)
-    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 4, 1]
+    # time with events (roofline), then one at a time without them (the plain one-lane latency)
+    assert [x[2] for x in r0["log"] if x[0] == "lanes"] == [4, 4, 1, 1]
     assert line["config"]["settle"]["frames"] >= 32 * 256 and line["config"]["settle"]["ms"] >= 60
     assert line["config"]["lanes"] == 4 and line["config"]["single_lane_ms_per_step"] > 0
     assert f0 and f1 and not (f0 & f1)
