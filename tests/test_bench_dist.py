@@ -196,7 +196,7 @@ def test_bench_line_fields_single_rank(monkeypatch):
     assert line["n_gpus"] == 1 and line["metric"] == "Mpixel/s encoded (4K PPM, q=90)"
     cfg = line["config"]
     assert cfg["input_slots"] == 12 and cfg["input_slots"] * 3840 * 2160 * 3 > 256 * 2**20  # past the MALL
-    assert cfg["single_lane_ms_per_step"] > 0
+    assert cfg["single_lane_ms_per_step"] > 0 and cfg["single_lane_plain_ms_per_step"] > 0
     rf = line["roofline"]
     assert rf["kernel"] == "k_emit" and rf["bound"] == "hbm" and rf["peak"] == 8000.0 and rf["unit"] == "GB/s"
     algo = 3840 * 2160 * 3 + 1000  # RGB in + the stand-in's JPEG bytes
