@@ -1,9 +1,10 @@
 """Per-kernel rocprofv3 durations of bench.py split into its passes.
 
 bench.py (default arguments) dispatches every k_* kernel S times in the untimed
-settle phase (config.settle.frames of its line), W + K times in the pipelined timed
-pass, then W + K times in the roofline pass (one frame at a
-time, HIP events around each launch).  rocprofv3 --stats averages all of them;
+settle phase (config.settle.frames / config.frames_per_step of its line), W + K
+times in the pipelined timed pass, W + K times in the roofline pass (one step at
+a time, HIP events around each launch), then K times in the plain one-lane pass
+(no events).  rocprofv3 --stats averages all of them;
 this splits run_kernel_trace.csv by dispatch order so the roofline pass's
 average can be compared with the `roofline.kernels[*].avg_launch_us` the bench
 line reports for the same dispatches.
@@ -21,7 +22,8 @@ if len(sys.argv) > 5:
     a = sys.argv[5]
     if a.endswith(".json"):  # the bench line of the same run: its settle frame count
         import json
-        S = int((json.load(open(a))["config"].get("settle") or {}).get("frames", 0))
+        cfg = json.load(open(a))["config"]  # (settle frames: launches x frames per step)
+        S = int((cfg.get("settle") or {}).get("frames", 0)) // max(1, int(cfg.get("frames_per_step", 1)))
     else:
         S = int(a)
 per = defaultdict(list)
@@ -32,7 +34,8 @@ for r in sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Dispatch_Id"])
 rows = []
 for name, d in per.items():
     n = W + K
-    passes = {"settle": d[:S], "timed_pipelined": d[S:S + n], "roofline_one_lane": d[S + n:S + 2 * n], "all": d}
+    passes = {"settle": d[:S], "timed_pipelined": d[S:S + n], "roofline_one_lane": d[S + n:S + 2 * n],
+              "plain_one_lane": d[S + 2 * n:S + 2 * n + K], "all": d}
     for p, v in passes.items():
         if v:
             rows.append({"kernel": name, "pass": p, "dispatches": len(v), "avg_us": round(sum(v) / len(v), 2),
